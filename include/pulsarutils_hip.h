@@ -1,0 +1,167 @@
+/*
+ * pulsarutils_hip.h - C-ABI of the MI355X (gfx950) dedispersion + cleaning library
+ * (libpulsarutils_hip.so).  Plain pointers and sizes only; no torch types.
+ *
+ * The reference (matteobachetti/radio-pulsar-utils, package ``pulsarutils``) is pure
+ * Python + numba; it has no FFI of its own.  Each entry point below replaces one
+ * reference function (cited file:line, paths relative to the reference root); the
+ * Python host layer (radio-pulsar-utils_amd/pulsarutils) binds them with ctypes
+ * exactly as INTEGRATION.md shows.
+ *
+ * Conventions
+ *  - Device pointers are owned by the caller (e.g. torch tensors).  Host pointers
+ *    are marked "host".  Row-major 2-D arrays carry a leading dimension ``ld``
+ *    (elements).
+ *  - Calls are asynchronous on ``stream`` (a hipStream_t passed as void*; NULL = the
+ *    null stream) and never throw.  They return PU_OK (0) or a negative PU_E* code;
+ *    pu_last_error() returns a thread-local message for the last failure.
+ *  - The caller selects the device (hipSetDevice) before calling.
+ */
+#ifndef PULSARUTILS_HIP_H
+#define PULSARUTILS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* element types */
+#define PU_U8 0
+#define PU_F32 1
+#define PU_F64 2
+#define PU_I64 3 /* rebin/roll helpers only */
+
+/* accumulation type of the dedispersion sum */
+#define PU_ACC_NATIVE 0 /* u8 -> f32 (exact), f32 -> f32, f64 -> f64 */
+#define PU_ACC_F32 1
+#define PU_ACC_F64 2 /* float64 accumulator in channel order: bit-exact vs the reference */
+
+/* status codes */
+#define PU_OK 0
+#define PU_EINVAL (-1)
+#define PU_EHIP (-2)
+#define PU_ENOMEM (-3)
+#define PU_EUNSUPPORTED (-4)
+
+const char *pu_version(void);
+const char *pu_last_error(void);
+
+/* ------------------------------------------------------------------ planner (host) */
+
+/* Replaces dedispersion_shifts (pulsarutils/dedispersion.py:125-139) for ``ndm``
+ * trials at once.  float64 with CPython scalar semantics (libm pow, float floor
+ * division, rint).  host: dms[ndm], out[ndm][nchan]. */
+int pu_shift_table(int64_t nchan, const double *dms, int64_t ndm, double start_freq,
+                   double bandwidth, double sample_time, int64_t *out);
+
+/* ------------------------------------------------------------------ dedispersion */
+
+typedef struct pu_plan pu_plan;
+
+/* Build a dedispersion plan for ``ndm`` trials over an (nchan, nsamples) filterbank
+ * of element type ``dtype``.  host: shifts[ndm][nchan] = the reference's per-channel
+ * integer delays (dedispersion_shifts output, any sign).  Tiles DM trials x time,
+ * derives per-tile LDS halos and uploads the metadata to the current device.
+ * Replaces the per-trial shift computation + normalize_shifts of
+ * _dedispersion_search (dedispersion.py:183-184, 97, 101-122). */
+int pu_plan_create(pu_plan **plan, int dtype, int acc, int64_t nchan, int64_t nsamples,
+                   const int64_t *shifts, int64_t ndm);
+void pu_plan_destroy(pu_plan *plan);
+
+/* Device scratch bytes pu_plan_search needs (per-tile partial statistics). */
+size_t pu_plan_workspace_bytes(const pu_plan *plan);
+
+/* Replaces _dedispersion_search (dedispersion.py:174-202): for every trial the
+ * circular shift-and-sum over channels, mean subtraction, and the S/N of the
+ * 1/2/4/8-sample rebinned series; outputs max, std, best snr, best rebin (device,
+ * [ndm] each).  data: device (nchan rows of ld elements). */
+int pu_plan_search(pu_plan *plan, const void *data, int64_t ld, double *max_out,
+                   double *std_out, double *snr_out, int32_t *rebin_out, void *workspace,
+                   size_t workspace_bytes, void *stream);
+
+/* Replaces dedisperse (dedispersion.py:93-98) for every trial of the plan: writes
+ * the dedispersed plane plane[trial * ld_plane + t] in the accumulation type
+ * (float32 or float64), the show=True plane of dedispersion_search (:214-227). */
+int pu_plan_dedisperse(pu_plan *plan, const void *data, int64_t ld, void *plane,
+                       int64_t ld_plane, void *stream);
+
+/* Measurement (bench.py): record a HIP event pair on the launch stream around each
+ * of the next ``nslots`` dedispersion-kernel launches of this plan (0 disables). */
+int pu_plan_enable_timing(pu_plan *plan, int nslots);
+/* Synchronises on the recorded events and writes up to ``n`` kernel durations (ms,
+ * launch order).  Returns the number written, or a negative PU_E* code. */
+int pu_plan_kernel_times(pu_plan *plan, float *ms, int n);
+
+/* Introspection (tests / DESIGN.md): fills up to ``n`` of
+ * {ndm, dm_tiles, time_tiles, trials_per_tile, time_tile, chans_per_step,
+ *  row_stride, lds_bytes, acc_is_f64, max_spread}. Returns the count written. */
+int pu_plan_info(const pu_plan *plan, int64_t *info, int n);
+
+/* ------------------------------------------------------------------ cleaning */
+
+/* Per-row sums in numpy's exact add.reduce order (8192-element blocks, each
+ * pairwise-summed), the reductions behind ndarray.mean(1) / np.std(axis=1) in
+ * get_noisier_channels (clean.py:60), measure_channel_variability (clean.py:119)
+ * and renormalize_data (clean.py:84).
+ *   mode 0: sum of x                     (acc: f32 for f32 input, else f64)
+ *   mode 1: sum of (x - center[r])^2     (center: device [nrows], acc type)
+ *   mode 2: sum of f64(x) * scale[t]     (scale: device [n] f64; acc f64)
+ * out: device [nrows] in the acc type; ``divisor`` > 0 divides each sum in float64
+ * and rounds to the acc type (numpy true_divide by the count). */
+int pu_row_sums(const void *x, int dtype, int64_t nrows, int64_t n, int64_t ld, int mode,
+                const void *center, const double *scale, double divisor, void *out,
+                void *workspace, size_t workspace_bytes, void *stream);
+size_t pu_row_sums_workspace_bytes(int64_t nrows, int64_t n);
+
+/* Column means over the rows with skip[r] == 0, sequential in row order
+ * (renormalize_data's zero-DM light curve, clean.py:77).  out: device [n] f64. */
+int pu_col_means(const void *x, int dtype, int64_t nrows, int64_t n, int64_t ld,
+                 const uint8_t *skip, double *out, void *stream);
+
+/* scipy.ndimage.gaussian_filter of a 1-D float64 series, mode 'reflect', in
+ * scipy's symmetric correlate1d order (clean.py:79).  weights: device [2r+1]. */
+int pu_gaussian_filter1d(const double *x, int64_t n, const double *weights, int64_t radius,
+                         double *out, void *stream);
+
+/* factor[t] = numerator / x[t] (clean.py:80). */
+int pu_ratio(double numerator, const double *x, int64_t n, double *out, void *stream);
+
+/* renormalize_data apply pass (clean.py:81-94): out[c][t] = bad[c] ? 0 :
+ * (f64(x[c][t]) * factor[t] - spec[c]) / spec[c]; if col_means != NULL it also
+ * writes the sequential column mean of ``out`` (the cut_outliers light curve). */
+int pu_renorm_apply(const void *x, int dtype, int64_t nchan, int64_t n, int64_t ld,
+                    const double *factor, const double *spec, const uint8_t *bad,
+                    double *out, int64_t ld_out, double *col_means, void *stream);
+
+/* out[:, cols[k]] = 0 for k < ncols (clean.py:105). cols: device int64. */
+int pu_zero_columns(double *out, int64_t nrows, int64_t ld_out, const int64_t *cols,
+                    int64_t ncols, void *stream);
+
+/* ------------------------------------------------------------------ rebin / roll */
+
+/* quick_resample (dedispersion.py:38-57): out[r][i] = 0 + sum_{j<w} x[r][i*w+j]
+ * in float64, i < n/w. */
+int pu_rebin_time(const void *x, int dtype, int64_t nrows, int64_t n, int64_t ld,
+                  int64_t rebin, double *out, void *stream);
+
+/* quick_chan_rebin (dedispersion.py:15-35): out[g][t] = sum_{j<r} x[g*r+j][t]
+ * sequentially; output type: f32->f32, f64->f64, u8->u64, i64->i64. */
+int pu_rebin_chan(const void *x, int dtype, int64_t nrows, int64_t n, int64_t ld,
+                  int64_t rebin, void *out, void *stream);
+
+/* apply_dm_shifts_to_data (dedispersion.py:254-258): out[c][t] =
+ * x[c][(t + shift[c]) mod n] (shift = rint of the reference shift; any sign). */
+int pu_roll_rows(const void *x, int dtype, int64_t nrows, int64_t n, int64_t ld,
+                 const int64_t *shifts, void *out, void *stream);
+
+/* roll_and_sum (dedispersion.py:60-83), in place on a float64 accumulator:
+ * sum[t] += f64(x[(t - roll) mod n]). */
+int pu_roll_and_sum(const void *x, int dtype, int64_t n, int64_t roll, double *sum,
+                    void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PULSARUTILS_HIP_H */

@@ -1,0 +1,224 @@
+"""ctypes binding of libpulsarutils_hip.so (the C-ABI in include/pulsarutils_hip.h).
+
+PyTorch-ROCm is plumbing here: device memory, the current HIP stream, host<->device
+copies.  Every compute step of the hot path is a call into the HIP library; there is
+no CPU fallback - without the library or a GPU the calls raise.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+PU_U8, PU_F32, PU_F64, PU_I64 = 0, 1, 2, 3
+PU_ACC_NATIVE, PU_ACC_F32, PU_ACC_F64 = 0, 1, 2
+_EINVAL, _EHIP, _ENOMEM, _EUNSUPPORTED = -1, -2, -3, -4
+
+_LIB_PATH = os.environ.get(
+    "PULSARUTILS_HIP_LIB",
+    os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libpulsarutils_hip.so"))
+
+_lib = None
+_lock = threading.Lock()
+
+# name -> (restype, argtypes)
+_i64, _i32, _f64, _vp, _sz = ctypes.c_int64, ctypes.c_int, ctypes.c_double, ctypes.c_void_p, ctypes.c_size_t
+SIGNATURES = {
+    "pu_version": (ctypes.c_char_p, []),
+    "pu_last_error": (ctypes.c_char_p, []),
+    "pu_shift_table": (_i32, [_i64, _vp, _i64, _f64, _f64, _f64, _vp]),
+    "pu_plan_create": (_i32, [ctypes.POINTER(_vp), _i32, _i32, _i64, _i64, _vp, _i64]),
+    "pu_plan_destroy": (None, [_vp]),
+    "pu_plan_workspace_bytes": (_sz, [_vp]),
+    "pu_plan_search": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "pu_plan_dedisperse": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp]),
+    "pu_plan_info": (_i32, [_vp, _vp, _i32]),
+    "pu_plan_enable_timing": (_i32, [_vp, _i32]),
+    "pu_plan_kernel_times": (_i32, [_vp, _vp, _i32]),
+    "pu_row_sums": (_i32, [_vp, _i32, _i64, _i64, _i64, _i32, _vp, _vp, _f64, _vp, _vp, _sz, _vp]),
+    "pu_row_sums_workspace_bytes": (_sz, [_i64, _i64]),
+    "pu_col_means": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp]),
+    "pu_gaussian_filter1d": (_i32, [_vp, _i64, _vp, _i64, _vp, _vp]),
+    "pu_ratio": (_i32, [_f64, _vp, _i64, _vp, _vp]),
+    "pu_renorm_apply": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
+    "pu_zero_columns": (_i32, [_vp, _i64, _i64, _vp, _i64, _vp]),
+    "pu_rebin_time": (_i32, [_vp, _i32, _i64, _i64, _i64, _i64, _vp, _vp]),
+    "pu_rebin_chan": (_i32, [_vp, _i32, _i64, _i64, _i64, _i64, _vp, _vp]),
+    "pu_roll_rows": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp]),
+    "pu_roll_and_sum": (_i32, [_vp, _i32, _i64, _i64, _vp, _vp]),
+}
+
+INFO_FIELDS = ("ndm", "dm_tiles", "time_tiles", "trials_per_tile", "time_tile", "chans_per_step",
+               "row_stride", "lds_bytes", "acc_is_f64", "max_spread")
+
+
+class HipBackendError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load the HIP library (raises if it is missing: no silent fallback)."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(_LIB_PATH):
+                    raise HipBackendError(
+                        f"pulsarutils: HIP library not found at {_LIB_PATH}; build it with "
+                        "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+                L = ctypes.CDLL(_LIB_PATH)
+                for name, (res, args) in SIGNATURES.items():
+                    fn = getattr(L, name)
+                    fn.restype = res
+                    fn.argtypes = args
+                _lib = L
+    return _lib
+
+
+def check(rc, what=""):
+    if rc == 0:
+        return
+    msg = lib().pu_last_error().decode(errors="replace")
+    if rc in (_EINVAL, _EUNSUPPORTED):
+        raise ValueError(f"{what}: {msg}")
+    if rc == _ENOMEM:
+        raise MemoryError(f"{what}: {msg}")
+    raise HipBackendError(f"{what}: {msg}")
+
+
+def torch():
+    import torch as _t
+    return _t
+
+
+def require_gpu():
+    t = torch()
+    if not t.cuda.is_available():
+        raise HipBackendError("pulsarutils: the dedispersion/cleaning path runs on a ROCm GPU "
+                              "(MI355X / gfx950); torch.cuda.is_available() is False")
+    lib()
+    return t
+
+
+def stream_ptr(stream=None):
+    t = torch()
+    s = stream if stream is not None else t.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def ptr(tensor):
+    return ctypes.c_void_p(tensor.data_ptr()) if tensor is not None else None
+
+
+_DTYPE_CODES = {}
+
+
+def dtype_code(tdtype):
+    t = torch()
+    if not _DTYPE_CODES:
+        _DTYPE_CODES.update({t.uint8: PU_U8, t.float32: PU_F32, t.float64: PU_F64, t.int64: PU_I64})
+    return _DTYPE_CODES.get(tdtype)
+
+
+def to_device(a, allowed=(PU_U8, PU_F32, PU_F64), device=None):
+    """numpy array or torch tensor -> contiguous device tensor of a supported dtype.
+
+    Unsupported element types are converted ON THE DEVICE to float64 (exact for
+    every integer below 2**53), i.e. the same promotion the reference's float64
+    accumulators apply.
+    """
+    t = require_gpu()
+    dev = device if device is not None else t.device("cuda", t.cuda.current_device())
+    if isinstance(a, t.Tensor):
+        x = a.to(dev)
+    else:
+        arr = np.asarray(a)
+        if arr.dtype == np.bool_:
+            arr = arr.astype(np.uint8)
+        if arr.dtype.byteorder not in ("=", "|"):
+            arr = arr.astype(arr.dtype.newbyteorder("="))
+        x = t.from_numpy(np.ascontiguousarray(arr)).to(dev, non_blocking=False)
+    if dtype_code(x.dtype) not in allowed:
+        x = x.to(t.float64)
+    return x.contiguous()
+
+
+class Plan:
+    """Owning wrapper of a ``pu_plan`` (dedispersion tiling + device metadata)."""
+
+    def __init__(self, dtype_code_, acc, nchan, nsamples, shifts):
+        require_gpu()
+        sh = np.ascontiguousarray(shifts, dtype=np.int64)
+        ndm = sh.shape[0]
+        assert sh.shape == (ndm, nchan)
+        h = ctypes.c_void_p()
+        check(lib().pu_plan_create(ctypes.byref(h), dtype_code_, acc, nchan, nsamples,
+                                   sh.ctypes.data_as(ctypes.c_void_p), ndm), "pu_plan_create")
+        self._h = h
+        self.dtype_code = dtype_code_
+        self.nchan, self.nsamples, self.ndm = nchan, nsamples, ndm
+        info = np.zeros(len(INFO_FIELDS), np.int64)
+        lib().pu_plan_info(h, info.ctypes.data_as(ctypes.c_void_p), len(INFO_FIELDS))
+        self.info = dict(zip(INFO_FIELDS, info.tolist()))
+        self.workspace_bytes = lib().pu_plan_workspace_bytes(h)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and _lib is not None:
+            _lib.pu_plan_destroy(h)
+            self._h = None
+
+    @property
+    def acc_is_f64(self):
+        return bool(self.info["acc_is_f64"])
+
+    def _check_data(self, data):
+        assert data.is_cuda and data.dim() == 2 and data.stride(1) == 1
+        assert tuple(data.shape) == (self.nchan, self.nsamples), (tuple(data.shape), self.nchan, self.nsamples)
+        assert dtype_code(data.dtype) == self.dtype_code
+
+    def search(self, data, out=None, workspace=None, stream=None):
+        """Launch the fused search; returns (max, std, snr, rebin) device tensors."""
+        t = torch()
+        self._check_data(data)
+        dev = data.device
+        if out is None:
+            out = (t.empty(self.ndm, dtype=t.float64, device=dev), t.empty(self.ndm, dtype=t.float64, device=dev),
+                   t.empty(self.ndm, dtype=t.float64, device=dev), t.empty(self.ndm, dtype=t.int32, device=dev))
+        if workspace is None:
+            workspace = t.empty(max(self.workspace_bytes, 16), dtype=t.uint8, device=dev)
+        check(lib().pu_plan_search(self._h, ptr(data), data.stride(0), ptr(out[0]), ptr(out[1]), ptr(out[2]),
+                                   ptr(out[3]), ptr(workspace), workspace.numel(), stream_ptr(stream)),
+              "pu_plan_search")
+        return out
+
+    def enable_timing(self, nslots):
+        check(lib().pu_plan_enable_timing(self._h, int(nslots)), "pu_plan_enable_timing")
+
+    def kernel_times_ms(self, n):
+        out = np.zeros(int(n), np.float32)
+        m = lib().pu_plan_kernel_times(self._h, out.ctypes.data_as(ctypes.c_void_p), int(n))
+        if m < 0:
+            check(m, "pu_plan_kernel_times")
+        return out[:m]
+
+    def dedisperse(self, data, plane=None, stream=None):
+        """Dedispersed plane (ndm, nsamples) in the accumulation dtype."""
+        t = torch()
+        self._check_data(data)
+        if plane is None:
+            plane = t.empty((self.ndm, self.nsamples), dtype=t.float64 if self.acc_is_f64 else t.float32,
+                            device=data.device)
+        check(lib().pu_plan_dedisperse(self._h, ptr(data), data.stride(0), ptr(plane), plane.stride(0),
+                                       stream_ptr(stream)), "pu_plan_dedisperse")
+        return plane
+
+
+def shift_table(nchan, trial_dms, start_freq, bandwidth, sample_time):
+    """pu_shift_table: the reference shifts for every trial, int64 [ndm, nchan] (host)."""
+    dms = np.ascontiguousarray(np.atleast_1d(np.asarray(trial_dms, dtype=np.float64)))
+    out = np.empty((dms.size, int(nchan)), np.int64)
+    check(lib().pu_shift_table(int(nchan), dms.ctypes.data_as(ctypes.c_void_p), dms.size, float(start_freq),
+                               float(bandwidth), float(sample_time), out.ctypes.data_as(ctypes.c_void_p)),
+          "pu_shift_table")
+    return out

@@ -1,0 +1,218 @@
+"""Drop-in ``pulsarutils.clean`` (reference: pulsarutils/clean.py) - the RFI-cleaning pass.
+
+The 2-D passes (per-channel means / standard deviations, the zero-DM light curve,
+the renormalisation and its column means) run in HIP kernels that reproduce numpy's
+exact reduction order, so the channel masks, the time-bin mask and the renormalised
+data are bit-identical to the reference (tests/test_gpu_clean.py).  The 1-D steps on
+nchan- or N-length vectors (medfilt, MAD, median, uniform_filter1d, quartiles) are
+host logic on the exact vectors the kernels return.
+
+``*_device`` variants take and return device tensors (no PCIe round trip of the
+2-D data) and are what the multi-GPU pipeline and the benchmark use.
+"""
+from dataclasses import dataclass
+
+import numpy as np
+from scipy.ndimage import uniform_filter1d
+from scipy.signal import medfilt
+
+from . import _hip
+from .dedispersion import (dedispersion_plan, dedispersion_shifts,  # noqa: F401
+                           apply_dm_shifts_to_data, quick_resample, quick_chan_rebin)
+from .dedispersion import dedispersion_search as fast_dedispersion_search  # noqa: F401
+from .stats import mad, ref_mad
+from .table import make_table
+
+
+@dataclass
+class PulseInfo():
+    """clean.py:27-55 container (no annotations: plain class attributes, as in the reference)."""
+    nbin = 0
+    nchan = 0
+    ph0 = None
+    amp = None
+    width = None
+    noise_level = None
+    dm = None
+    pulse_freq = None
+    start_freq = None
+    bandwidth = None
+    dedisp_profile = None
+    allprofs = None
+    disp_profile = None
+
+    disp_z2 = None
+    disp_z6 = None
+    disp_z12 = None
+    disp_z20 = None
+    disp_H = None
+    disp_M = None
+
+    dedisp_z2 = None
+    dedisp_z6 = None
+    dedisp_z12 = None
+    dedisp_z20 = None
+    dedisp_H = None
+    dedisp_M = None
+
+
+# ---------------------------------------------------------------- device reductions
+
+def _row_sums(x, mode, center=None, scale=None, divisor=0.0):
+    t = _hip.torch()
+    code = _hip.dtype_code(x.dtype)
+    acc_f32 = code == _hip.PU_F32 and mode != 2
+    nrows, n = x.shape
+    out = t.empty(nrows, dtype=t.float32 if acc_f32 else t.float64, device=x.device)
+    ws = t.empty(max(16, _hip.lib().pu_row_sums_workspace_bytes(nrows, n)), dtype=t.uint8, device=x.device)
+    _hip.check(_hip.lib().pu_row_sums(_hip.ptr(x), code, nrows, n, x.stride(0), mode, _hip.ptr(center),
+                                      _hip.ptr(scale), float(divisor), _hip.ptr(out), _hip.ptr(ws), ws.numel(),
+                                      _hip.stream_ptr()), "pu_row_sums")
+    return out
+
+
+def channel_means_device(x):
+    """``x.mean(1)`` with numpy's dtype and summation order (float32 stays float32)."""
+    return _row_sums(x, 0, divisor=x.shape[1])
+
+
+def channel_variances_device(x, means=None):
+    """``np.var(x, axis=1)`` (ddof 0) in numpy's order; ``np.std`` = host ``np.sqrt`` of it."""
+    if means is None:
+        means = channel_means_device(x)
+    return _row_sums(x, 1, center=means, divisor=x.shape[1])
+
+
+def _host(t):
+    return t.detach().cpu().numpy()
+
+
+def get_noisier_channels(array):
+    """clean.py:58-67: channels whose mean exceeds medfilt(spec, 7) + 5 ref_mad."""
+    x = _hip.to_device(array)
+    spec = _host(channel_means_device(x))
+    smooth_spec = medfilt(spec, 7)
+    return spec > smooth_spec + 5 * ref_mad(spec)
+
+
+def measure_channel_variability(array, badchans_mask=None):
+    """clean.py:114-133: per-channel std outside [q2 - 2(q2-q1), q2 + 2(q3-q2)].
+
+    Quartile positions use the full channel count, as in the reference (an
+    IndexError when too many channels are masked is the reference behaviour).
+    """
+    x = _hip.to_device(array)
+    spec = np.sqrt(_host(channel_variances_device(x)))
+    if badchans_mask is None:
+        badchans_mask = np.zeros(spec.size, dtype=bool)
+    badchans_mask = np.asarray(badchans_mask, dtype=bool)
+    ordered = np.sort(spec[~badchans_mask])
+    q1 = ordered[spec.size // 4]
+    q2 = ordered[spec.size // 2]
+    q3 = ordered[spec.size // 4 * 3]
+    lowlim = q2 - 2 * (q2 - q1)
+    hilim = q2 + 2 * (q3 - q2)
+    return (spec < lowlim) | (spec > hilim) | badchans_mask
+
+
+def _gaussian_weights(sigma):
+    from scipy.ndimage._filters import _gaussian_kernel1d
+    radius = int(4.0 * float(sigma) + 0.5)
+    return np.ascontiguousarray(_gaussian_kernel1d(sigma, 0, radius)[::-1]), radius
+
+
+def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=False, out=None):
+    """renormalize_data on a device tensor; returns (float64 device tensor, bad_bins or None).
+
+    Passes (clean.py:73-105): zero-DM light curve over good channels (column means,
+    rows in order) -> gaussian_filter (GPU, scipy's order) -> host median -> factor
+    -> per-channel mean of x*factor (numpy pairwise order) -> (x*f - mu)/mu with bad
+    channels zeroed [+ its column mean] -> host uniform_filter1d(16) thresholds ->
+    zero the bad time bins.
+    """
+    t = _hip.torch()
+    nchan, n = x.shape
+    dev = x.device
+    code = _hip.dtype_code(x.dtype)
+    lib = _hip.lib()
+    s = _hip.stream_ptr()
+    if badchans_mask is None:
+        badchans_mask = np.zeros(nchan, dtype=bool)
+    bad_np = np.ascontiguousarray(np.asarray(badchans_mask, dtype=bool)).astype(np.uint8)
+    bad = t.from_numpy(bad_np).to(dev)
+    lc = t.empty(n, dtype=t.float64, device=dev)
+    _hip.check(lib.pu_col_means(_hip.ptr(x), code, nchan, n, x.stride(0), _hip.ptr(bad), _hip.ptr(lc), s),
+               "pu_col_means")
+    sigma = min(baseline_window, n // 100 * 2 + 1)
+    w, radius = _gaussian_weights(sigma)
+    dw = t.from_numpy(w).to(dev)
+    smooth = t.empty(n, dtype=t.float64, device=dev)
+    _hip.check(lib.pu_gaussian_filter1d(_hip.ptr(lc), n, _hip.ptr(dw), radius, _hip.ptr(smooth), s),
+               "pu_gaussian_filter1d")
+    med = float(np.median(_host(smooth)))
+    factor = t.empty(n, dtype=t.float64, device=dev)
+    _hip.check(lib.pu_ratio(med, _hip.ptr(smooth), n, _hip.ptr(factor), s), "pu_ratio")
+    spec = _row_sums(x, 2, scale=factor, divisor=n)
+    if out is None:
+        out = t.empty((nchan, n), dtype=t.float64, device=dev)
+    col = t.empty(n, dtype=t.float64, device=dev) if cut_outliers else None
+    _hip.check(lib.pu_renorm_apply(_hip.ptr(x), code, nchan, n, x.stride(0), _hip.ptr(factor), _hip.ptr(spec),
+                                   _hip.ptr(bad), _hip.ptr(out), out.stride(0), _hip.ptr(col), s),
+               "pu_renorm_apply")
+    bad_bins = None
+    if cut_outliers:
+        lc2 = _host(col)
+        window = 16  # only the last window of the reference loop (range(0, 5)) survives
+        lc_rebin = uniform_filter1d(lc2, window)
+        thresh_up = 5 * np.std(lc_rebin[::window])
+        thresh_down = -3 * np.std(lc_rebin[::window])
+        bad_bins = (lc_rebin > + thresh_up) | (lc_rebin < thresh_down)
+        cols = np.nonzero(bad_bins)[0].astype(np.int64)
+        if cols.size:
+            dcols = t.from_numpy(cols).to(dev)
+            _hip.check(lib.pu_zero_columns(_hip.ptr(out), nchan, out.stride(0), _hip.ptr(dcols), cols.size, s),
+                       "pu_zero_columns")
+    return out, bad_bins
+
+
+def renormalize_data(array, diagnostic_figure=None, badchans_mask=None, baseline_window=101,
+                     cut_outliers=False):
+    """clean.py:70-111: zero-DM normalisation + per-channel (x - mu)/mu, float64 out."""
+    x = _hip.to_device(array)
+    out, _ = renormalize_device(x, badchans_mask=badchans_mask, baseline_window=baseline_window,
+                                cut_outliers=cut_outliers)
+    return _host(out)
+
+
+def dedispersion_search(info, dmmin, dmmax):
+    """clean.py:136-180: plane search of a PulseInfo -> (plane, Table).
+
+    sample_time = 1 / pulse_freq / nbin.  The plane is float64 (ndm, N) in memory
+    (the reference writes it to ``dummy.npy`` in the CWD; not reproduced).  The
+    rebin column is int64 as in the reference.
+    """
+    from .dedispersion import dedispersion_search as dsearch
+    data = info.allprofs
+    sample_time = 1 / info.pulse_freq / info.nbin
+    table, plane = dsearch(data, dmmin, dmmax, info.start_freq, info.bandwidth, sample_time, show=True)
+    return plane, table
+
+
+def digitize(data):
+    """clean.py:183-189 (diagnostics): MAD-scaled, clipped, rounded integers."""
+    if isinstance(data, (int, np.integer)):
+        return data
+    std = mad(data)
+    data = (data - np.median(data)) / std * 3
+    data[data < 0] = 0
+    return np.rint(data).astype(int)
+
+
+def dm_broadening(dm, freq, df):
+    """clean.py:272-273: intra-channel DM smearing (s)."""
+    return 8300 * dm * df / freq**3
+
+
+__all__ = ["PulseInfo", "get_noisier_channels", "renormalize_data", "measure_channel_variability",
+           "dedispersion_search", "digitize", "dm_broadening", "renormalize_device",
+           "channel_means_device", "channel_variances_device", "make_table"]

@@ -1,0 +1,80 @@
+"""HIP cleaning parity (GPU): channel masks, time-bin masks and renormalised data are
+bit-exact against the reference's own outputs (goldens) and the numpy oracle."""
+import hashlib
+from dataclasses import replace
+
+import numpy as np
+import pytest
+
+from oracle import clean_oracle as co
+from pulsarutils import clean as C
+from pulsarutils import synth
+from pulsarutils.configs import CONFIGS
+
+pytestmark = pytest.mark.gpu
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def check_case(golden, tag, x):
+    arrays, meta = golden
+    assert sha(x) == meta[f"{tag}_input_sha256"]
+    import torch
+    from pulsarutils import _hip
+    xd = _hip.to_device(x)
+    means = C.channel_means_device(xd).cpu().numpy()
+    np.testing.assert_array_equal(means, arrays[f"{tag}_spec_mean"])
+    std = np.sqrt(C.channel_variances_device(xd).cpu().numpy())
+    np.testing.assert_array_equal(std, arrays[f"{tag}_spec_std"])
+    bad = C.get_noisier_channels(x)
+    np.testing.assert_array_equal(bad, arrays[f"{tag}_noisier"])
+    np.testing.assert_array_equal(C.measure_channel_variability(x), arrays[f"{tag}_variability"])
+    np.testing.assert_array_equal(C.measure_channel_variability(x, badchans_mask=bad),
+                                  arrays[f"{tag}_variability_masked"])
+    for cut in (False, True):
+        key = f"{tag}_renorm_{'cut' if cut else 'nocut'}"
+        out, bins = C.renormalize_device(xd, badchans_mask=bad, cut_outliers=cut)
+        ren = out.cpu().numpy()
+        if sha(ren) != meta[key + "_sha256"]:
+            ref = co.renormalize(x, badchans_mask=bad, cut_outliers=cut)
+            diff = np.argwhere(ren != ref)
+            pytest.fail(f"{key}: {len(diff)} elements differ, first {diff[:5].tolist()}")
+        if cut:
+            expect = arrays[key + "_badbins"]
+            np.testing.assert_array_equal(np.nonzero(bins)[0], expect)
+        del out
+        torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("dt", ["f32", "u8", "f64"])
+def test_clean_ragged(gpu, golden, dt):
+    rag = replace(CONFIGS["C4"], nchan=100, nsamples=12345, seed=77)
+    check_case(golden, f"rag{dt}", synth.rfi_filterbank_np(rag, dtype=dt))
+
+
+@pytest.mark.parametrize("dt", ["f32", "u8"])
+def test_clean_c4_bitexact(gpu, golden, dt):
+    check_case(golden, f"c4{dt}", synth.rfi_filterbank_np(CONFIGS["C4"], dtype=dt))
+
+
+def test_clean_c1_float64(gpu, golden):
+    arrays, meta = golden
+    from test_gpu_dedisperse import c1_input
+    x = c1_input()
+    bad = C.get_noisier_channels(x)
+    np.testing.assert_array_equal(bad, arrays["c1_noisier"])
+    np.testing.assert_array_equal(C.measure_channel_variability(x), arrays["c1_variability"])
+    ren = C.renormalize_data(x, badchans_mask=bad, cut_outliers=True)
+    assert sha(ren) == meta["c1_renorm_cut_sha256"]
+
+
+def test_renormalize_api_matches_oracle_small(gpu):
+    rng = np.random.default_rng(9)
+    x = (rng.random((20, 700)) * 5 + 1).astype(np.float32)
+    bad = np.zeros(20, bool)
+    bad[[3, 7]] = True
+    np.testing.assert_array_equal(C.renormalize_data(x, badchans_mask=bad, cut_outliers=True),
+                                  co.renormalize(x, badchans_mask=bad, cut_outliers=True))
+    np.testing.assert_array_equal(C.renormalize_data(x), co.renormalize(x))

@@ -1,0 +1,253 @@
+"""HIP dedispersion parity (GPU): through the C-ABI, against the oracle and the goldens.
+
+Tolerances:
+* float64 accumulation (acc='f64', and float64 input by default): bit-exact series.
+* uint8 input, float32 accumulation: bit-exact (all partial sums are integers < 2**24).
+* float32 input, float32 accumulation: |gpu - ref| <= nchan * 2**-24 * sum_c |x_c| per sample.
+* search statistics: max/std/snr within 1e-5 relative (1e-9 for float64 accumulation);
+  argmax DM and rebin equal unless the top two S/N are within that tolerance.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+import oracle
+from pulsarutils import dedispersion as D
+from pulsarutils import simulate, _hip
+from pulsarutils.configs import CONFIGS
+
+pytestmark = pytest.mark.gpu
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def c1_input():
+    c = CONFIGS["C1"]
+    np.random.seed(c.seed)
+    arr, _ = simulate.simulate_test_data(dm=c.pulse_dm, tsamp=c.tsamp, nsamples=c.nsamples, nchan=c.nchan,
+                                         start_freq=c.start_freq, bandwidth=c.bandwidth)
+    return arr
+
+
+def f32_bound(x, shifts):
+    """Per-sample first-order bound nchan * 2^-24 * sum_c |x_c[(t+s_c) mod N]|."""
+    ax = np.abs(x.astype(np.float64))
+    return x.shape[0] * 2.0 ** -24 * oracle.dedisperse(ax, shifts) + 1e-30
+
+
+# ------------------------------------------------------------------ doctests / helpers
+
+def test_doctest_quick_chan_rebin(gpu, golden):
+    counts = np.array([np.arange(0, 10), np.arange(2, 12), np.arange(1, 11), np.arange(3, 13),
+                       np.arange(1, 11), np.arange(3, 13)])
+    reb = D.quick_chan_rebin(counts, 2)
+    assert reb.dtype == golden[0]["doctest_chan_rebin"].dtype
+    np.testing.assert_array_equal(reb, golden[0]["doctest_chan_rebin"])
+
+
+def test_doctest_quick_resample(gpu, golden):
+    counts = np.array([np.arange(1, 11), np.arange(3, 13)])
+    np.testing.assert_array_equal(D.quick_resample(counts, 2), golden[0]["doctest_resample"])
+
+
+def test_doctest_roll_and_sum_in_place(gpu, golden):
+    array = np.arange(10)
+    sum_array = np.zeros(10)
+    assert np.allclose(D.roll_and_sum(array, sum_array, 3), np.roll(array, 3))
+    assert sum_array is D.roll_and_sum(array, sum_array, 3)
+    np.testing.assert_array_equal(sum_array, 2 * golden[0]["doctest_roll_and_sum"])
+
+
+def test_rebin_roll_goldens(gpu, golden):
+    arrays, _ = golden
+    x = arrays["rebin_in"]
+    for r in (1, 2, 3, 8):
+        np.testing.assert_array_equal(D.quick_resample(x, r), arrays[f"resample_{r}"])
+        np.testing.assert_array_equal(D.quick_chan_rebin(x, r), arrays[f"chanrebin_{r}"])
+        np.testing.assert_array_equal(D.quick_chan_rebin(x.astype(np.float32), r),
+                                      x.astype(np.float32)[:x.shape[0] // r * r].reshape(-1, r, x.shape[1]).sum(1))
+    np.testing.assert_array_equal(D.apply_dm_shifts_to_data(x, arrays["roll_shifts"]), arrays["roll_out"])
+    u = (x * 255).astype(np.uint8)
+    np.testing.assert_array_equal(D.quick_chan_rebin(u, 3), u[:6].reshape(2, 3, -1).sum(1))
+    np.testing.assert_array_equal(D.apply_dm_shifts_to_data(u, arrays["roll_shifts"]),
+                                  np.array([np.roll(u[i], -int(np.rint(s))) for i, s in
+                                            enumerate(arrays["roll_shifts"])]))
+
+
+# ------------------------------------------------------------------ dedisperse
+
+def test_dedisperse_bitexact_c1_rows(gpu, golden):
+    arrays, meta = golden
+    c = CONFIGS["C1"]
+    arr = c1_input()
+    for k, i in enumerate(arrays["c1_dedisp_rows_idx"]):
+        sh = D.dedispersion_shifts(c.nchan, arrays["plan_C1"][i], c.start_freq, c.bandwidth, c.tsamp)
+        dd = D.dedisperse(arr, sh)
+        assert dd.dtype == np.float64
+        assert sha(dd) == meta[f"c1_dedisp_sha256_{i}"]
+
+
+@pytest.mark.parametrize("dt", ["u8", "f32", "f64"])
+@pytest.mark.parametrize("shape", [(1, 7), (3, 100), (17, 1000), (64, 4099), (33, 65536)])
+def test_dedisperse_random_shapes_exact_f64(gpu, dt, shape):
+    rng = np.random.default_rng(shape[0] * 1000 + shape[1])
+    nchan, n = shape
+    x = {"u8": lambda: rng.integers(0, 256, shape).astype(np.uint8),
+         "f32": lambda: rng.standard_normal(shape).astype(np.float32),
+         "f64": lambda: rng.standard_normal(shape)}[dt]()
+    sh = rng.integers(-3 * n, 3 * n, nchan).astype(float)
+    np.testing.assert_array_equal(D.dedisperse(x, sh), oracle.dedisperse(x, sh.astype(np.int64)))
+
+
+def _plane(x, shifts, acc):
+    t = _hip.require_gpu()
+    xd = _hip.to_device(x)
+    plan = _hip.Plan(_hip.dtype_code(xd.dtype), D._acc_code(acc), x.shape[0], x.shape[1], shifts)
+    return plan.dedisperse(xd).cpu().numpy()
+
+
+@pytest.mark.parametrize("name", ["C1", "C5"])
+def test_plane_native_vs_oracle(gpu, golden, name):
+    arrays, _ = golden
+    c = CONFIGS[name]
+    rng = np.random.default_rng(11)
+    n = min(c.nsamples, 1 << 15)
+    x = np.abs(rng.standard_normal((c.nchan, n))).astype(np.float32) * 0.5
+    dms = arrays[f"plan_{name}"]
+    idx = np.linspace(0, dms.size - 1, 40).astype(int)
+    sh = _hip.shift_table(c.nchan, dms[idx], c.start_freq, c.bandwidth, c.tsamp)
+    plane = _plane(x, sh, "native")
+    assert plane.dtype == np.float32
+    for k in range(len(idx)):
+        ref = oracle.dedisperse(x, sh[k])
+        assert np.all(np.abs(plane[k] - ref) <= f32_bound(x, sh[k])), k
+    u = (x * 100).astype(np.uint8)
+    pu = _plane(u, sh, "native")
+    for k in range(0, len(idx), 5):
+        np.testing.assert_array_equal(pu[k].astype(np.float64), oracle.dedisperse(u, sh[k]))
+    p64 = _plane(x, sh, "f64")
+    for k in range(0, len(idx), 7):
+        np.testing.assert_array_equal(p64[k], oracle.dedisperse(x, sh[k]))
+
+
+def test_plane_arbitrary_dm_list_large_spread(gpu):
+    """Non-plan trial lists (random order, huge shift spreads): tile splitting + halo."""
+    rng = np.random.default_rng(5)
+    nchan, n = 48, 5000
+    x = rng.standard_normal((nchan, n))
+    sh = rng.integers(-20000, 20000, (70, nchan))
+    plane = _plane(x, sh, "f64")
+    for k in range(70):
+        np.testing.assert_array_equal(plane[k], oracle.dedisperse(x, sh[k]))
+
+
+# ------------------------------------------------------------------ search tables
+
+def test_search_test_config_vs_reference(gpu, golden):
+    arrays, meta = golden
+    np.random.seed(0)
+    arr, h = simulate.simulate_test_data(150)
+    assert sha(arr) == meta["test_input_sha256"]
+    tab = D.dedispersion_search(arr, 100, 200., h["fbottom"], h["bandwidth"], h["tsamp"])
+    np.testing.assert_array_equal(tab["DM"], arrays["test_table_DM"])
+    for col in ("max", "std", "snr"):
+        np.testing.assert_allclose(tab[col], arrays[f"test_table_{col}"], rtol=1e-9, atol=1e-12)
+    np.testing.assert_array_equal(tab["rebin"], arrays["test_table_rebin"])
+    assert tab["rebin"].dtype == np.int32
+    # the reference test's assertion (tests/test_dedispersion.py:25)
+    assert np.isclose(tab["DM"][np.argmax(tab["snr"])], 150, atol=1)
+
+
+def test_search_slow_path_plane(gpu, golden):
+    arrays, meta = golden
+    np.random.seed(0)
+    arr, h = simulate.simulate_test_data(150)
+    tab, plane = D.dedispersion_search(arr, 100, 200., h["fbottom"], h["bandwidth"], h["tsamp"], show=True)
+    assert sha(plane) == meta["test_plane_sha256"]
+    assert tab["rebin"].dtype == np.int64
+    np.testing.assert_array_equal(tab["rebin"], arrays["test_slow_table_rebin"])
+    np.testing.assert_allclose(tab["snr"], arrays["test_slow_table_snr"], rtol=1e-9)
+    assert np.isclose(tab["DM"][np.argmax(tab["snr"])], 150, atol=1)
+
+
+def test_search_c1_vs_reference(gpu, golden):
+    arrays, _ = golden
+    c = CONFIGS["C1"]
+    arr = c1_input()
+    mx, sd, snr, win = D._dedispersion_search(arr, arrays["plan_C1"], c.nchan, c.start_freq, c.bandwidth, c.tsamp)
+    np.testing.assert_allclose(mx, arrays["c1_table_max"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(sd, arrays["c1_table_std"], rtol=1e-9)
+    np.testing.assert_allclose(snr, arrays["c1_table_snr"], rtol=1e-9)
+    np.testing.assert_array_equal(win, arrays["c1_table_rebin"])
+    assert win.dtype == np.int32
+
+
+@pytest.mark.parametrize("acc", ["native", "f32"])
+def test_search_c1_float32_accumulation(gpu, golden, acc):
+    arrays, _ = golden
+    c = CONFIGS["C1"]
+    arr = c1_input()
+    mx, sd, snr, win = D._dedispersion_search(arr, arrays["plan_C1"], c.nchan, c.start_freq, c.bandwidth, c.tsamp,
+                                              acc="f32" if acc == "f32" else None)
+    tol = 1e-5 if acc == "f32" else 1e-9
+    np.testing.assert_allclose(snr, arrays["c1_table_snr"], rtol=tol)
+    np.testing.assert_allclose(sd, arrays["c1_table_std"], rtol=tol)
+
+
+@pytest.mark.parametrize("dt", ["f32", "u8"])
+def test_search_ragged_small(gpu, dt):
+    """Tiny / ragged inputs: N smaller than a time tile, odd nchan, N % 8 != 0."""
+    rng = np.random.default_rng(3)
+    for nchan, n in [(3, 37), (5, 200), (31, 1001), (130, 3000)]:
+        x = rng.random((nchan, n)) * 10
+        x = x.astype(np.float32) if dt == "f32" else x.astype(np.uint8)
+        dms = np.linspace(0, 300, 23)
+        g = D._dedispersion_search(x, dms, nchan, 400., 100., 1e-3)
+        o = oracle.search(x, dms, 400., 100., 1e-3)
+        for a, b in zip(g[:3], o[:3]):
+            np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-9)
+        np.testing.assert_array_equal(g[3], o[3])
+
+
+@pytest.mark.parametrize("name", ["C2", "C5"])
+def test_search_full_size_sampled_trials(gpu, golden, name):
+    """Full-size configs on device data; a spread of trials re-done by the C oracle."""
+    import torch
+    from pulsarutils import synth
+    arrays, _ = golden
+    c = CONFIGS[name]
+    xd = synth.pulsar_filterbank_device(c)
+    dms = arrays[f"plan_{name}"]
+    (mx, sd, snr, win), plan = D.search_device(xd, dms, c.nchan, c.start_freq, c.bandwidth, c.tsamp)
+    torch.cuda.synchronize()
+    snr = snr.cpu().numpy()
+    best = dms[np.argmax(snr)]
+    assert abs(best - c.pulse_dm) < 0.5, (best, c.pulse_dm)
+    x = xd.cpu().numpy()
+    idx = np.unique(np.r_[np.linspace(0, dms.size - 1, 6).astype(int), np.argmax(snr)])
+    omx, osd, osnr, owin = oracle.search(x, dms[idx], c.start_freq, c.bandwidth, c.tsamp, nthreads=16)
+    np.testing.assert_allclose(snr[idx], osnr, rtol=1e-5)
+    np.testing.assert_allclose(sd.cpu().numpy()[idx], osd, rtol=1e-5)
+    np.testing.assert_allclose(mx.cpu().numpy()[idx], omx, rtol=1e-4, atol=1e-3)
+    np.testing.assert_array_equal(win.cpu().numpy()[idx], owin)
+
+
+def test_search_u8_bitexact_series_c3_slice(gpu):
+    """uint8 C3-like slice: float32 accumulation is exact -> plane equals the float64 oracle."""
+    import torch
+    from dataclasses import replace
+    from pulsarutils import synth
+    c = replace(CONFIGS["C3"], nsamples=1 << 16)
+    xd = synth.pulsar_filterbank_device(c)
+    dms = D.dedispersion_plan(c.nchan, c.dmmin, c.dmmax, c.start_freq, c.bandwidth, c.tsamp)
+    idx = np.linspace(0, dms.size - 1, 5).astype(int)
+    sh = _hip.shift_table(c.nchan, dms[idx], c.start_freq, c.bandwidth, c.tsamp)
+    plan = _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, c.nchan, c.nsamples, sh)
+    plane = plan.dedisperse(xd).cpu().numpy()
+    x = xd.cpu().numpy()
+    for k in range(len(idx)):
+        np.testing.assert_array_equal(plane[k].astype(np.float64), oracle.dedisperse(x, sh[k]))
+    torch.cuda.synchronize()
