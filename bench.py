@@ -74,7 +74,7 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--acc", default="native", choices=["native", "f32", "f64"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-trials", type=int, default=48)
+    ap.add_argument("--cpu-trials", type=int, default=400)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
