@@ -6,38 +6,45 @@
 //
 // out_d[t] = sum_c x[c][(t + s[d][c]) mod N]   (s = dedispersion_shifts, any sign)
 //
-// Mapping (DESIGN.md §3):
-//   * one workgroup = 4 waves = one DM tile (4*D trials) x one time tile (64*K samples);
-//     each wave owns D trials, lane l owns samples t0 + l + 64k, k < K  -> D*K
-//     accumulators in VGPRs.
-//   * channel rows are staged in LDS, ncc channels per step, each row covering
-//     [t0 + smin_c, t0 + 64K + smax_c) mod N: the modular halo of the tile.
-//   * per (channel, trial) the shift relative to smin_c is wave-uniform (SGPR); the
-//     K-sample window is re-read from LDS only when it changes from the previous
-//     trial (adjacent plan trials differ by <= 1 sample per channel), so most adds
-//     reuse registers: LDS traffic ~ (1 + (D-1)|slope_c|)/D dwords per add.
-//   * accumulation in channel order 0..nchan-1, like the reference; with a float64
-//     accumulator the series is bit-identical to the reference's.
-//   * epilogue: either the dedispersed plane (coalesced stores), or per-tile partial
-//     statistics of the 1/2/4/8-sample rebinned series (max, shifted sum, shifted
-//     sum of squares) reduced by pu_finalize_kernel in a fixed order.
-//   * blockIdx is remapped XCD-aware so all DM tiles of a time tile run on one XCD
-//     and share the staged input through its L2.
+// Mapping (DESIGN.md §4.1):
+//   * one workgroup = 8 waves = one DM tile (64 trials) x one time tile; each wave
+//     owns D = 8 trials, lane l owns K samples (float: t0 + 2l + 128j + e, j<4, e<2)
+//     -> D*K accumulators in VGPRs.
+//   * channel rows are staged in LDS, ncc channels per chunk, each row covering
+//     [t0 + smin_c, t0 + TT + smax_c) mod N: the tile's modular halo.  Rows arrive by
+//     LDS-DMA (global_load_lds, 1 KiB pieces, per-lane modular addresses only for
+//     the rare windows that wrap) into a two-buffer ring: chunk k+1 lands while chunk
+//     k is summed.  Converting inputs (u8, f64 -> f32 LDS) use register staging.
+//   * per (tile, channel, wave) the host precomputes 8 x u16 "window records": the LDS
+//     byte offset of each trial's K-sample window (alignment copy included) and, in
+//     bit 15, whether it differs from the previous trial's.  One scalar load per
+//     channel; per trial one s_bitcmp1 + branch; the window is re-read (in place, 4 x
+//     ds_read_b64) only when it changes -- adjacent plan trials differ by <= 1 sample
+//     per channel, so most v_add_f32 reuse registers.  The first window of the next
+//     channel is prefetched into the other window buffer while this one is summed.
+//   * accumulation in channel order 0..nchan-1 (reference order: with a float64
+//     accumulator the series is bit-identical).
+//   * epilogue: the dedispersed plane, or per-tile partial statistics of the
+//     1/2/4/8-sample rebinned series reduced by pu_finalize_kernel in a fixed order.
+//   * blockIdx is remapped XCD-aware so all DM tiles of a time tile run on one XCD.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "pu_common.h"
 
 namespace {
 
-constexpr int kWaves = 4;
+constexpr int kWaves = 8;                 // waves per workgroup (each owns D trials)
 constexpr int kThreads = kWaves * 64;
-constexpr int kPartStride = 16;  // doubles per (trial, time tile) partial record
-constexpr size_t kLdsBudget = 32 * 1024;
+constexpr int kD = 8;                     // trials per wave
+constexpr int kTPT = kWaves * kD;         // trials per tile
+constexpr int kPartStride = 16;           // doubles per (trial, time tile) partial record
+constexpr size_t kLdsBudget = 48 * 1024;  // both ring buffers: 3 workgroups / CU
 constexpr int kMaxSpread = 2048;
 
 struct DedispArgs {
@@ -68,11 +75,19 @@ __device__ __forceinline__ T shfl_xor(T v, int d)
     return __shfl_xor(v, d, 64);
 }
 
-// Read one K-sample window of a staged row into registers: J = 4 ds_read_b64 at
-// 512-byte strides (lane l gets 8 contiguous bytes of each 512-byte slice).  Written
-// as one asm block that overwrites the window in place, so the register allocator
-// never keeps two windows alive (the reuse branch would otherwise make phi copies),
-// and that waits for its own LDS reads.
+// Uniform (scalar-cache) load: the constant address space makes hipcc emit s_load.
+template <typename T>
+__device__ __forceinline__ T ld_uniform(const T *p)
+{
+    return *(const __attribute__((address_space(4))) T *)(p);
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// In-place K-sample window read: 4 x ds_read_b64 at 512-byte strides + wait.  One asm
+// block that overwrites the window registers, so the register allocator never keeps
+// two versions alive.  Outputs are early-clobber: an LDS read can return (and write
+// its destination) before the block's later reads have consumed the address VGPR.
 __device__ __forceinline__ void read_window(double (&w)[4], uint32_t addr)
 {
     asm volatile(
@@ -81,9 +96,28 @@ __device__ __forceinline__ void read_window(double (&w)[4], uint32_t addr)
         "ds_read_b64 %2, %4 offset:1024\n\t"
         "ds_read_b64 %3, %4 offset:1536\n\t"
         "s_waitcnt lgkmcnt(0)"
-        : "=v"(w[0]), "=v"(w[1]), "=v"(w[2]), "=v"(w[3])
+        : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3])
         : "v"(addr)
         : "memory");
+}
+
+// Same reads without the wait (prefetch of the next channel's first window); the
+// registers are only consumed after wait_window() on them.
+__device__ __forceinline__ void prefetch_window(double (&w)[4], uint32_t addr)
+{
+    asm volatile(
+        "ds_read_b64 %0, %4\n\t"
+        "ds_read_b64 %1, %4 offset:512\n\t"
+        "ds_read_b64 %2, %4 offset:1024\n\t"
+        "ds_read_b64 %3, %4 offset:1536"
+        : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3])
+        : "v"(addr)
+        : "memory");
+}
+
+__device__ __forceinline__ void wait_window(double (&w)[4])
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]) : : "memory");
 }
 
 // Empty asm that "uses" one trial's accumulators: keeps each trial's adds ahead of the
@@ -110,23 +144,37 @@ __device__ __forceinline__ Tl window_elem(const double (&w)[4], int k)
     }
 }
 
-// Kernel geometry per lane: E = 8 / sizeof(Tl) consecutive samples per 8-byte LDS
-// read, J = 4 reads per window, K = E*J samples per lane:
-//   sample(l, j, e) = t0 + E*l + 64*E*j + e.
-// float rows are staged twice (copy q holds row[start + q + i]) so every 8-byte read
-// is aligned whatever the parity of the shift.
-template <typename Tin, typename Tl, typename Ta, int D, bool PLANE, bool STATS>
+// Add one channel's contribution to all D trials of this wave.  ``rec`` = 8 u16
+// window records (byte offset | reload flag << 15); ``w`` holds trial 0's window.
+template <typename Tl, typename Ta, int K>
+__device__ __forceinline__ void channel_trials(Ta (&acc)[kD][K], double (&w)[4], const u32x4 rec, uint32_t cbase)
+{
+#pragma unroll
+    for (int d = 0; d < kD; ++d) {
+        if (d > 0) {
+            const uint32_t word = rec[d >> 1] >> (16 * (d & 1));
+            if (word & 0x8000u) read_window(w, cbase + (word & 0x7fffu));
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc[d][k] += static_cast<Ta>(window_elem<Tl>(w, k));
+        pin_accumulators(acc[d]);
+    }
+}
+
+template <typename Tin, typename Tl, typename Ta, bool PLANE, bool STATS>
 __global__ void __launch_bounds__(kThreads)
-dedisp_kernel(DedispArgs a, const int32_t *__restrict__ tile_first,
-              const int32_t *__restrict__ tile_count, const int32_t *__restrict__ tile_rowlen,
-              const int32_t *__restrict__ base_tab, const uint16_t *__restrict__ rel_tab)
+dedisp_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const int32_t *__restrict__ tile_count,
+              const int32_t *__restrict__ tile_rowlen, const int32_t *__restrict__ base_tab,
+              const u32x4 *__restrict__ rec_tab)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int E = 8 / (int)sizeof(Tl);
-    constexpr int J = 4;
-    constexpr int K = E * J;
-    constexpr int TT = 64 * K;
-    constexpr int TPT = kWaves * D;  // trials per tile
+    constexpr bool kDma = std::is_same<Tin, Tl>::value;
+    constexpr int SZ = (int)sizeof(Tl);
+    constexpr int E = 8 / SZ;     // samples per 8-byte LDS read
+    constexpr int J = 4;          // reads per window
+    constexpr int K = E * J;      // samples per lane
+    constexpr int TT = 64 * K;    // samples per time tile
+    constexpr int D = kD;
 
     const int wg = pu::xcd_remap(blockIdx.x, gridDim.x);
     const int dt = wg % a.ndt;
@@ -135,20 +183,18 @@ dedisp_kernel(DedispArgs a, const int32_t *__restrict__ tile_first,
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int first = tile_first[dt];
-    const int cnt = tile_count[dt];
-    const int rowlen = tile_rowlen[dt];
+    const int first = ld_uniform(tile_first + dt);
+    const int cnt = ld_uniform(tile_count + dt);
+    const int rowlen = ld_uniform(tile_rowlen + dt);
     const int slot0 = wave * D;
     const bool active = slot0 < cnt;
     const int n = a.n;
-    const int stride = a.row_stride;            // elements per copy (even)
-    const int chan_bytes = E * stride * (int)sizeof(Tl);
-    // LDS: [rel: ncc x TPT u16][rows: ncc x E copies x stride]
-    uint16_t *lds_rel = reinterpret_cast<uint16_t *>(smem);
-    const int rel_bytes = (a.ncc * TPT * 2 + 15) & ~15;
-    Tl *lds_rows = reinterpret_cast<Tl *>(smem + rel_bytes);
-    const uint32_t rows_addr = (uint32_t)(uintptr_t)lds_rows;
-    const uint32_t lane_addr = rows_addr + 8u * lane;
+    const int stride = a.row_stride;           // elements per row copy
+    const int copy_bytes = stride * SZ;
+    const int chan_bytes = E * copy_bytes;
+    const int buf_bytes = a.ncc * chan_bytes;
+    // LDS byte address of the dynamic region (local-address-space pointer -> 32-bit offset)
+    const uint32_t smem_addr = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char *)smem;
 
     Ta acc[D][K];
 #pragma unroll
@@ -157,20 +203,64 @@ dedisp_kernel(DedispArgs a, const int32_t *__restrict__ tile_first,
         for (int k = 0; k < K; ++k) acc[d][k] = Ta(0);
 
     const int32_t *base = base_tab + (size_t)dt * a.nchan;
-    const uint16_t *rel = rel_tab + (size_t)dt * a.nchan * TPT;
+    const u32x4 *recs = rec_tab + (size_t)dt * a.nchan * kWaves + wave;
     const Tin *data = reinterpret_cast<const Tin *>(a.data);
+    const int nchunks = (a.nchan + a.ncc - 1) / a.ncc;
+    // bytes of a row copy actually moved (whole 256-byte pieces)
+    const int cover_bytes = (rowlen * SZ + 255) & ~255;
+    const int cover = cover_bytes / SZ;
 
-    for (int c0 = 0; c0 < a.nchan; c0 += a.ncc) {
+    // ---- LDS-DMA of chunk k into ring buffer b: each wave moves whole row copies
+    auto issue_dma = [&](int k, int b) {
+        const int c0 = k * a.ncc;
         const int nc = min(a.ncc, a.nchan - c0);
-        __syncthreads();
-        // ---- stage: relative shifts of the chunk, then E copies of each row window
-        for (int e = tid; e < nc * TPT; e += kThreads) lds_rel[e] = rel[(size_t)c0 * TPT + e];
+        const uint32_t bufo = (uint32_t)(b * buf_bytes);
+        for (int r = wave; r < nc * E; r += kWaves) {
+            const int ci = r / E, q = r % E;
+            const int c = c0 + ci;
+            const char *row = reinterpret_cast<const char *>(data + (size_t)c * (size_t)a.ld);
+            int start = ld_uniform(base + c) + t0 + q;
+            if (start >= n) start -= n;
+            if (start >= n) start -= n;
+            unsigned char *dst = smem + bufo + ci * chan_bytes + q * copy_bytes;
+            if (!a.small_n && start + cover <= n) {
+                // contiguous window: 1 KiB pieces (16 B/lane), then 256 B pieces
+                const char *src = row + (size_t)start * SZ;
+                int off = 0;
+                for (; off + 1024 <= cover_bytes; off += 1024)
+                    __builtin_amdgcn_global_load_lds((const void *)(src + off + 16 * lane),
+                                                     (__attribute__((address_space(3))) void *)(dst + off), 16, 0, 0);
+                for (; off < cover_bytes; off += 256)
+                    __builtin_amdgcn_global_load_lds((const void *)(src + off + 4 * lane),
+                                                     (__attribute__((address_space(3))) void *)(dst + off), 4, 0, 0);
+            } else {
+                // wrapping window: per-lane modular element index, 4 B per lane
+                for (int off = 0; off < cover_bytes; off += 256) {
+                    const int byte = off + 4 * lane;
+                    int idx = start + byte / SZ;
+                    if (!a.small_n) {
+                        idx = idx >= n ? idx - n : idx;
+                    } else {
+                        idx %= n;
+                    }
+                    const char *src = row + (size_t)idx * SZ + (byte % SZ);
+                    __builtin_amdgcn_global_load_lds((const void *)src,
+                                                     (__attribute__((address_space(3))) void *)(dst + off), 4, 0, 0);
+                }
+            }
+        }
+    };
+
+    // ---- register staging for converting inputs (u8 -> f32, f64 -> f32)
+    auto stage_regs = [&](int k) {
+        const int c0 = k * a.ncc;
+        const int nc = min(a.ncc, a.nchan - c0);
         for (int ci = 0; ci < nc; ++ci) {
             const int c = c0 + ci;
             const Tin *row = data + (size_t)c * (size_t)a.ld;
-            int start = base[c] + t0;
+            int start = ld_uniform(base + c) + t0;
             if (start >= n) start -= n;
-            Tl *dst = lds_rows + (size_t)ci * E * stride;
+            Tl *dst = reinterpret_cast<Tl *>(smem + ci * chan_bytes);
             const int len = rowlen + E - 1;
             for (int j = tid; j < len; j += kThreads) {
                 int idx = start + j;
@@ -186,34 +276,44 @@ dedisp_kernel(DedispArgs a, const int32_t *__restrict__ tile_first,
                 }
             }
         }
-        __syncthreads();
+    };
+
+    if constexpr (kDma) issue_dma(0, 0);
+    for (int k = 0; k < nchunks; ++k) {
+        const int c0 = k * a.ncc;
+        const int nc = min(a.ncc, a.nchan - c0);
+        const int b = kDma ? (k & 1) : 0;
+        __syncthreads();  // this wave's DMA landed (vmcnt) and every wave left the other buffer
+        if constexpr (kDma) {
+            if (k + 1 < nchunks) issue_dma(k + 1, b ^ 1);
+        } else {
+            stage_regs(k);
+            __syncthreads();
+        }
         if (!active) continue;
-        // ---- accumulate: per channel, D trials x K samples, window reused while the
-        // (wave-uniform) shift does not change from one trial to the next
-        for (int ci = 0; ci < nc; ++ci) {
-            const uint32_t *rr32 = reinterpret_cast<const uint32_t *>(lds_rel + ci * TPT + slot0);
-            uint32_t rw[D / 2];
-#pragma unroll
-            for (int q = 0; q < D / 2; ++q) rw[q] = __builtin_amdgcn_readfirstlane(rr32[q]);
-            const uint32_t cbase = lane_addr + (uint32_t)(ci * chan_bytes);
-            double w[4];
-            int prev = -1;
-#pragma unroll
-            for (int d = 0; d < D; ++d) {
-                const int s = (int)((rw[d >> 1] >> (16 * (d & 1))) & 0xffffu);
-                if (d == 0 || s != prev) {
-                    uint32_t off;
-                    if constexpr (E == 2)
-                        off = (uint32_t)((s & 1) * stride * 4 + (s & ~1) * 4);
-                    else
-                        off = (uint32_t)(s * 8);
-                    read_window(w, cbase + off);
-                    prev = s;
-                }
-#pragma unroll
-                for (int k = 0; k < K; ++k) acc[d][k] += static_cast<Ta>(window_elem<Tl>(w, k));
-                pin_accumulators(acc[d]);
-            }
+        // ---- accumulate the chunk: channel pairs alternate window buffers so the next
+        // channel's first window is read while this one is summed
+        const uint32_t rows_lane = smem_addr + (uint32_t)(b * buf_bytes) + 8u * lane;
+        double w0[4], w1[4];
+        const u32x4 *rc = recs + (size_t)c0 * kWaves;
+        u32x4 rec0 = ld_uniform(rc);
+        u32x4 rec1 = nc > 1 ? ld_uniform(rc + kWaves) : rec0;
+        read_window(w0, rows_lane + (rec0[0] & 0x7fffu));
+        for (int ci = 0; ci < nc; ci += 2) {
+            const uint32_t cb0 = rows_lane + (uint32_t)(ci * chan_bytes);
+            const bool has1 = ci + 1 < nc, has2 = ci + 2 < nc, has3 = ci + 3 < nc;
+            u32x4 rec2 = rec0, rec3 = rec1;
+            if (has2) rec2 = ld_uniform(rc + (size_t)(ci + 2) * kWaves);  // two channels ahead
+            if (has1) prefetch_window(w1, cb0 + chan_bytes + (rec1[0] & 0x7fffu));
+            channel_trials<Tl, Ta, K>(acc, w0, rec0, cb0);
+            if (!has1) break;
+            wait_window(w1);
+            if (has3) rec3 = ld_uniform(rc + (size_t)(ci + 3) * kWaves);
+            if (has2) prefetch_window(w0, cb0 + 2 * chan_bytes + (rec2[0] & 0x7fffu));
+            channel_trials<Tl, Ta, K>(acc, w1, rec1, cb0 + chan_bytes);
+            if (has2) wait_window(w0);
+            rec0 = rec2;
+            rec1 = rec3;
         }
     }
     if (!active) return;
@@ -235,23 +335,24 @@ dedisp_kernel(DedispArgs a, const int32_t *__restrict__ tile_first,
         }
     }
     if constexpr (STATS) {
+        // Per trial: lane-local stats of the 1/2/4/8-sample rebinned sums in the
+        // accumulation type (few terms), then float64 wave reductions.
 #pragma unroll
         for (int d = 0; d < D; ++d) {
             if (slot0 + d >= cnt) break;
-            const double kt = static_cast<double>(__shfl(acc[d][0], 0, 64));
-            double mx[4], s1[4], s2[4];
+            const Ta kt = __shfl(acc[d][0], 0, 64);
+            Ta mx[4], s1[4], s2[4];
 #pragma unroll
             for (int w = 0; w < 4; ++w) {
                 mx[w] = -INFINITY;
-                s1[w] = 0.0;
-                s2[w] = 0.0;
+                s1[w] = Ta(0);
+                s2[w] = Ta(0);
             }
             auto account = [&](int w, Ta r, int t, bool lane_ok) {
                 const int width = 1 << w;
                 if (lane_ok && t + width <= n) {
-                    const double rv = static_cast<double>(r);
-                    const double y = rv - width * kt;
-                    mx[w] = fmax(mx[w], rv);
+                    const Ta y = r - Ta(width) * kt;
+                    mx[w] = fmax(mx[w], r);
                     s1[w] += y;
                     s2[w] += y * y;
                 }
@@ -280,25 +381,24 @@ dedisp_kernel(DedispArgs a, const int32_t *__restrict__ tile_first,
                     }
                 }
             }
+            double* p = a.partials + ((size_t)(first + slot0 + d) * a.ntt + tt) * kPartStride;
 #pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
+            for (int w = 0; w < 4; ++w) {
+                Ta m = mx[w];
+                double x1 = static_cast<double>(s1[w]), x2 = static_cast<double>(s2[w]);
 #pragma unroll
-                for (int w = 0; w < 4; ++w) {
-                    mx[w] = fmax(mx[w], shfl_xor(mx[w], off));
-                    s1[w] += shfl_xor(s1[w], off);
-                    s2[w] += shfl_xor(s2[w], off);
+                for (int off = 32; off > 0; off >>= 1) {
+                    m = fmax(m, shfl_xor(m, off));
+                    x1 += shfl_xor(x1, off);
+                    x2 += shfl_xor(x2, off);
+                }
+                if (lane == 0) {
+                    p[1 + 3 * w] = static_cast<double>(m);
+                    p[2 + 3 * w] = x1;
+                    p[3 + 3 * w] = x2;
                 }
             }
-            if (lane == 0) {
-                double *p = a.partials + ((size_t)(first + slot0 + d) * a.ntt + tt) * kPartStride;
-                p[0] = kt;
-#pragma unroll
-                for (int w = 0; w < 4; ++w) {
-                    p[1 + 3 * w] = mx[w];
-                    p[2 + 3 * w] = s1[w];
-                    p[3 + 3 * w] = s2[w];
-                }
-            }
+            if (lane == 0) p[0] = static_cast<double>(kt);
         }
     }
 }
@@ -374,20 +474,21 @@ pu_finalize_kernel(const double *__restrict__ part, int ntt, int n, int tt_len,
     }
 }
 
+
 enum Variant { V_U8_F32, V_F32_F32, V_F64_F64, V_U8_F64, V_F32_F64, V_F64_F32, V_COUNT };
 
 struct VariantInfo {
-    int D, K, lds_elem, acc_f64;
+    int lds_elem, acc_f64, dma;
 };
 
-// D trials per wave; K samples per lane = (8 / LDS element size) * 4 reads
+// K samples per lane = (8 / LDS element size) * 4 reads; D = 8 trials per wave
 constexpr VariantInfo kVariants[V_COUNT] = {
-    {8, 8, 4, 0},  // u8 in, f32 LDS, f32 acc (exact: sums < 2^24)
-    {8, 8, 4, 0},  // f32
-    {8, 4, 8, 1},  // f64 in, f64 LDS, f64 acc (bit-exact vs reference)
-    {8, 8, 4, 1},  // u8 in, f32 LDS, f64 acc
-    {8, 8, 4, 1},  // f32 in, f32 LDS, f64 acc (bit-exact vs reference)
-    {8, 8, 4, 0},  // f64 in, f32 LDS, f32 acc
+    {4, 0, 0},  // u8 in, f32 LDS (register staging), f32 acc (exact: sums < 2^24)
+    {4, 0, 1},  // f32 in, f32 LDS (DMA), f32 acc
+    {8, 1, 1},  // f64 in, f64 LDS (DMA), f64 acc (bit-exact vs reference)
+    {4, 1, 0},  // u8 in, f32 LDS, f64 acc
+    {4, 1, 1},  // f32 in, f32 LDS (DMA), f64 acc (bit-exact vs reference)
+    {4, 0, 0},  // f64 in, f32 LDS (register staging), f32 acc
 };
 
 int pick_variant(int dtype, int acc)
@@ -400,19 +501,16 @@ int pick_variant(int dtype, int acc)
     }
 }
 
-template <typename Tin, typename Tl, typename Ta, int D>
-int launch_variant(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s);
-
 }  // namespace
 
 struct pu_plan {
     int dtype = 0, acc = 0, variant = 0;
     int64_t nchan = 0, n = 0, ndm = 0;
-    int D = 0, K = 0, TT = 0, tpt = 0;  // trials per tile
+    int K = 0, TT = 0;
     int ndt = 0, ntt = 0, ncc = 0, row_stride = 0, small_n = 0, max_spread = 0;
     size_t lds_bytes = 0;
     int32_t *d_first = nullptr, *d_count = nullptr, *d_rowlen = nullptr, *d_base = nullptr;
-    uint16_t *d_rel = nullptr;
+    u32x4 *d_rec = nullptr;
     // optional kernel timing: event pairs recorded around each dedispersion launch
     std::vector<hipEvent_t> ev_start, ev_stop;
     int64_t launches = 0;
@@ -420,28 +518,44 @@ struct pu_plan {
 
 namespace {
 
-template <typename Tin, typename Tl, typename Ta, int D>
+template <typename Kern>
+int ensure_lds(Kern kern, size_t bytes)
+{
+    if (bytes <= 64 * 1024) return PU_OK;
+    return pu::hip_check(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes),
+                         "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
+}
+
+template <typename Tin, typename Tl, typename Ta>
 int launch_variant(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
 {
     const dim3 grid((unsigned)((int64_t)p->ndt * p->ntt)), block(kThreads);
-    if (plane)
-        hipLaunchKernelGGL((dedisp_kernel<Tin, Tl, Ta, D, true, false>), grid, block, p->lds_bytes, s,
-                           a, p->d_first, p->d_count, p->d_rowlen, p->d_base, p->d_rel);
-    else
-        hipLaunchKernelGGL((dedisp_kernel<Tin, Tl, Ta, D, false, true>), grid, block, p->lds_bytes, s,
-                           a, p->d_first, p->d_count, p->d_rowlen, p->d_base, p->d_rel);
+    if (plane) {
+        auto kern = dedisp_kernel<Tin, Tl, Ta, true, false>;
+        int rc = ensure_lds(kern, p->lds_bytes);
+        if (rc) return rc;
+        hipLaunchKernelGGL(kern, grid, block, p->lds_bytes, s, a, p->d_first, p->d_count, p->d_rowlen, p->d_base,
+                           p->d_rec);
+    } else {
+        auto kern = dedisp_kernel<Tin, Tl, Ta, false, true>;
+        int rc = ensure_lds(kern, p->lds_bytes);
+        if (rc) return rc;
+        hipLaunchKernelGGL(kern, grid, block, p->lds_bytes, s, a, p->d_first, p->d_count, p->d_rowlen, p->d_base,
+                           p->d_rec);
+    }
     return pu::launch_check("dedisp_kernel");
 }
 
 int dispatch_variant(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
 {
     switch (p->variant) {
-    case V_U8_F32: return launch_variant<uint8_t, float, float, 8>(p, a, plane, s);
-    case V_F32_F32: return launch_variant<float, float, float, 8>(p, a, plane, s);
-    case V_F64_F64: return launch_variant<double, double, double, 8>(p, a, plane, s);
-    case V_U8_F64: return launch_variant<uint8_t, float, double, 8>(p, a, plane, s);
-    case V_F32_F64: return launch_variant<float, float, double, 8>(p, a, plane, s);
-    case V_F64_F32: return launch_variant<double, float, float, 8>(p, a, plane, s);
+    case V_U8_F32: return launch_variant<uint8_t, float, float>(p, a, plane, s);
+    case V_F32_F32: return launch_variant<float, float, float>(p, a, plane, s);
+    case V_F64_F64: return launch_variant<double, double, double>(p, a, plane, s);
+    case V_U8_F64: return launch_variant<uint8_t, float, double>(p, a, plane, s);
+    case V_F32_F64: return launch_variant<float, float, double>(p, a, plane, s);
+    case V_F64_F32: return launch_variant<double, float, float>(p, a, plane, s);
     }
     pu::set_error("bad plan variant");
     return PU_EINVAL;
@@ -468,8 +582,17 @@ void free_plan(pu_plan *p)
     (void)hipFree(p->d_count);
     (void)hipFree(p->d_rowlen);
     (void)hipFree(p->d_base);
-    (void)hipFree(p->d_rel);
+    (void)hipFree(p->d_rec);
     delete p;
+}
+
+template <typename T>
+int upload(T **dst, const std::vector<T> &vec)
+{
+    const size_t bytes = vec.size() * sizeof(T);
+    int rc = pu::hip_check(hipMalloc((void **)dst, std::max<size_t>(bytes, 16)), "hipMalloc(plan)");
+    if (rc) return rc;
+    return pu::hip_check(hipMemcpy(*dst, vec.data(), bytes, hipMemcpyHostToDevice), "hipMemcpy(plan)");
 }
 
 }  // namespace
@@ -499,16 +622,15 @@ int pu_plan_create(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t n, 
     p->nchan = nchan;
     p->n = n;
     p->ndm = ndm;
-    p->D = kVariants[v].D;
-    p->K = kVariants[v].K;
-    p->TT = 64 * p->K;
-    p->tpt = kWaves * p->D;
     const int esz = kVariants[v].lds_elem;
+    const int E = 8 / esz;
+    p->K = E * 4;
+    p->TT = 64 * p->K;
 
-    // ---- greedy DM tiles: up to tpt consecutive trials whose per-channel shift
+    // ---- greedy DM tiles: up to kTPT consecutive trials whose per-channel shift
     // spread (max - min) stays <= kMaxSpread
     std::vector<int32_t> first, count, rowlen, base;
-    std::vector<uint16_t> rel;
+    std::vector<int32_t> rel;  // [tile][channel][slot] shift - smin (mod n)
     std::vector<int64_t> mn((size_t)nchan), mx((size_t)nchan);
     int64_t i = 0;
     int max_rowlen = 0;
@@ -516,7 +638,7 @@ int pu_plan_create(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t n, 
         const int64_t *s0 = shifts + i * nchan;
         for (int64_t c = 0; c < nchan; ++c) mn[c] = mx[c] = s0[c];
         int64_t j = i + 1;
-        while (j < ndm && j - i < p->tpt) {
+        while (j < ndm && j - i < kTPT) {
             const int64_t *sj = shifts + j * nchan;
             bool ok = true;
             for (int64_t c = 0; c < nchan; ++c) {
@@ -538,15 +660,16 @@ int pu_plan_create(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t n, 
         count.push_back(cntt);
         int spread = 0;
         const size_t rbase = rel.size();
-        rel.resize(rbase + (size_t)nchan * p->tpt, 0);
+        rel.resize(rbase + (size_t)nchan * kTPT, 0);
         for (int64_t c = 0; c < nchan; ++c) {
             int64_t b = mn[c] % n;
             if (b < 0) b += n;
             base.push_back((int32_t)b);
-            for (int s = 0; s < cntt; ++s) {
-                int64_t r = (shifts[(i + s) * nchan + c] - mn[c]) % n;  // >= 0
-                rel[rbase + (size_t)c * p->tpt + s] = (uint16_t)r;
-                spread = std::max(spread, (int)r);
+            int32_t *rr = rel.data() + rbase + (size_t)c * kTPT;
+            for (int s = 0; s < kTPT; ++s) {
+                const int ss = s < cntt ? s : cntt - 1;  // padding slots repeat the last trial
+                rr[s] = (int32_t)((shifts[(i + ss) * nchan + c] - mn[c]) % n);
+                spread = std::max(spread, (int)rr[s]);
             }
         }
         p->max_spread = std::max(p->max_spread, spread);
@@ -557,36 +680,51 @@ int pu_plan_create(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t n, 
     }
     p->ndt = (int)first.size();
     p->ntt = (int)((n + p->TT - 1) / p->TT);
-    const int ecopies = 8 / esz;  // float rows are staged twice (8-byte aligned pair reads)
-    p->row_stride = (max_rowlen + 3) & ~3;
-    // one wrap per staged index needs rowlen + 1 <= n
-    p->small_n = (int64_t)max_rowlen + 1 > n ? 1 : 0;
-    const size_t per_chan = (size_t)ecopies * p->row_stride * esz + (size_t)p->tpt * 2;
-    p->ncc = (int)std::max<int64_t>(1, std::min<int64_t>(nchan, (int64_t)(kLdsBudget / per_chan)));
-    p->lds_bytes = (((size_t)p->ncc * p->tpt * 2 + 15) & ~(size_t)15) + (size_t)p->ncc * ecopies * p->row_stride * esz;
+    const int epp = 256 / esz;  // elements per 256-byte DMA piece
+    // register staging writes rowlen + E - 1 elements; DMA moves whole 256-byte pieces
+    p->row_stride = (max_rowlen + E + epp - 1) / epp * epp;
+    p->small_n = (int64_t)p->row_stride + 2 > n ? 1 : 0;
+    const int nbuf = kVariants[v].dma ? 2 : 1;
+    const size_t chan_bytes = (size_t)E * p->row_stride * esz;
+    p->ncc = (int)std::max<int64_t>(1, std::min<int64_t>(nchan, (int64_t)(kLdsBudget / nbuf / chan_bytes)));
+    p->lds_bytes = nbuf * (size_t)p->ncc * chan_bytes;
+
+    // ---- window records: per (tile, channel, wave) 8 x u16 = LDS byte offset of each
+    // trial's window inside the channel slot | (window differs from the previous trial) << 15
+    const size_t copy_bytes = (size_t)p->row_stride * esz;
+    std::vector<u32x4> rec((size_t)p->ndt * nchan * kWaves);
+    for (size_t t = 0; t < (size_t)p->ndt; ++t)
+        for (int64_t c = 0; c < nchan; ++c)
+            for (int w = 0; w < kWaves; ++w) {
+                const int32_t *rr = rel.data() + (t * nchan + c) * kTPT + w * kD;
+                uint32_t words[kD];
+                uint32_t prev = 0xffffffffu;
+                for (int d = 0; d < kD; ++d) {
+                    const uint32_t s = (uint32_t)rr[d];
+                    const uint32_t off = E == 2 ? (uint32_t)((s & 1u) * copy_bytes + (s & ~1u) * 4u) : s * 8u;
+                    words[d] = off | (off != prev ? 0x8000u : 0u);
+                    prev = off;
+                }
+                u32x4 r;
+                for (int q = 0; q < 4; ++q) r[q] = words[2 * q] | (words[2 * q + 1] << 16);
+                rec[(t * nchan + c) * kWaves + w] = r;
+            }
     if ((int64_t)p->ndt * p->ntt >= (int64_t(1) << 31)) {
         free_plan(p);
         pu::set_error("pu_plan_create: grid too large");
         return PU_EINVAL;
     }
-    if (p->lds_bytes > 64 * 1024) {
+    if (2 * copy_bytes > 32768 || p->lds_bytes > 160 * 1024) {
         free_plan(p);
         pu::set_error("pu_plan_create: LDS row of %d elements does not fit", p->row_stride);
         return PU_EUNSUPPORTED;
     }
-
-    auto upload = [](auto **dst, const auto &vec) -> int {
-        const size_t bytes = vec.size() * sizeof(vec[0]);
-        int rc = pu::hip_check(hipMalloc((void **)dst, std::max<size_t>(bytes, 16)), "hipMalloc(plan)");
-        if (rc) return rc;
-        return pu::hip_check(hipMemcpy(*dst, vec.data(), bytes, hipMemcpyHostToDevice), "hipMemcpy(plan)");
-    };
     int rc = PU_OK;
     if (!rc) rc = upload(&p->d_first, first);
     if (!rc) rc = upload(&p->d_count, count);
     if (!rc) rc = upload(&p->d_rowlen, rowlen);
     if (!rc) rc = upload(&p->d_base, base);
-    if (!rc) rc = upload(&p->d_rel, rel);
+    if (!rc) rc = upload(&p->d_rec, rec);
     if (rc) {
         free_plan(p);
         return rc;
@@ -633,7 +771,7 @@ size_t pu_plan_workspace_bytes(const pu_plan *p)
 int pu_plan_info(const pu_plan *p, int64_t *info, int n)
 {
     if (!p || !info) return 0;
-    const int64_t v[] = {p->ndm, p->ndt, p->ntt, p->tpt, p->TT, p->ncc,
+    const int64_t v[] = {p->ndm, p->ndt, p->ntt, kTPT, p->TT, p->ncc,
                          p->row_stride, (int64_t)p->lds_bytes, kVariants[p->variant].acc_f64, p->max_spread};
     const int m = std::min<int>(n, (int)(sizeof v / sizeof v[0]));
     for (int k = 0; k < m; ++k) info[k] = v[k];
