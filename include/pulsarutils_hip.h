@@ -108,6 +108,8 @@ int pu_plan_info(const pu_plan *plan, int64_t *info, int n);
  *   mode 0: sum of x                     (acc: f32 for f32 input, else f64)
  *   mode 1: sum of (x - center[r])^2     (center: device [nrows], acc type)
  *   mode 2: sum of f64(x) * scale[t]     (scale: device [n] f64; acc f64)
+ *   mode 3: sum of f64(x)                (acc f64 for every input type)
+ *   mode 4: sum of f64(x)^2              (acc f64; get_spectral_stats, stats.py:46-47)
  * out: device [nrows] in the acc type; ``divisor`` > 0 divides each sum in float64
  * and rounds to the acc type (numpy true_divide by the count). */
 int pu_row_sums(const void *x, int dtype, int64_t nrows, int64_t n, int64_t ld, int mode,
@@ -160,6 +162,12 @@ int pu_roll_rows(const void *x, int dtype, int64_t nrows, int64_t n, int64_t ld,
  * sum[t] += f64(x[(t - roll) mod n]). */
 int pu_roll_and_sum(const void *x, int dtype, int64_t n, int64_t roll, double *sum,
                     void *stream);
+
+/* (rows, cols) -> (cols, rows) transpose of 1/2/4/8-byte elements: the time-major ->
+ * channel-major reordering sigpyproc's FilReader.readBlock performs on SIGPROC data
+ * (clean.py:327, stats.py:45).  dst[c * ld_dst + r] = src[r * ld_src + c]. */
+int pu_transpose(const void *src, int elem_bytes, int64_t rows, int64_t cols, int64_t ld_src,
+                 void *dst, int64_t ld_dst, void *stream);
 
 #ifdef __cplusplus
 }

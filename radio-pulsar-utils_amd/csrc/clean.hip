@@ -42,6 +42,9 @@ __device__ __forceinline__ Ta load_val(const Tin *row, int64_t t, Ta center, con
     } else if constexpr (MODE == 1) {
         const Ta d = static_cast<Ta>(row[t]) - center;
         return d * d;
+    } else if constexpr (MODE == 4) {
+        const Ta v = static_cast<Ta>(row[t]);
+        return v * v;
     } else {
         return static_cast<Ta>(static_cast<double>(row[t]) * scale[t]);
     }
@@ -250,6 +253,8 @@ int row_sums_in(int mode, bool f32acc, const void *x, int64_t nrows, int64_t n, 
                 const double *scale, double divisor, void *out, void *ws, hipStream_t s)
 {
     if (mode == 2) return row_sums_t<Tin, double, 2>(x, nrows, n, ld, center, scale, divisor, out, ws, s);
+    if (mode == 3) return row_sums_t<Tin, double, 0>(x, nrows, n, ld, center, scale, divisor, out, ws, s);
+    if (mode == 4) return row_sums_t<Tin, double, 4>(x, nrows, n, ld, center, scale, divisor, out, ws, s);
     if (f32acc) {
         if (mode == 0) return row_sums_t<Tin, float, 0>(x, nrows, n, ld, center, scale, divisor, out, ws, s);
         return row_sums_t<Tin, float, 1>(x, nrows, n, ld, center, scale, divisor, out, ws, s);
@@ -275,7 +280,7 @@ int pu_row_sums(const void *x, int dtype, int64_t nrows, int64_t n, int64_t ld, 
 {
     PU_REQUIRE(x && out, "pu_row_sums: NULL pointer");
     PU_REQUIRE(nrows > 0 && n > 0 && ld >= n, "pu_row_sums: bad shape");
-    PU_REQUIRE(mode >= 0 && mode <= 2, "pu_row_sums: bad mode %d", mode);
+    PU_REQUIRE(mode >= 0 && mode <= 4, "pu_row_sums: bad mode %d", mode);
     PU_REQUIRE(mode != 1 || center, "pu_row_sums: mode 1 needs center");
     PU_REQUIRE(mode != 2 || scale, "pu_row_sums: mode 2 needs scale");
     PU_REQUIRE(ws && ws_bytes >= pu_row_sums_workspace_bytes(nrows, n), "pu_row_sums: workspace too small");

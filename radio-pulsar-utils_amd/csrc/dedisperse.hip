@@ -31,6 +31,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 #include <vector>
@@ -686,7 +687,10 @@ int pu_plan_create(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t n, 
     p->small_n = (int64_t)p->row_stride + 2 > n ? 1 : 0;
     const int nbuf = kVariants[v].dma ? 2 : 1;
     const size_t chan_bytes = (size_t)E * p->row_stride * esz;
-    p->ncc = (int)std::max<int64_t>(1, std::min<int64_t>(nchan, (int64_t)(kLdsBudget / nbuf / chan_bytes)));
+    // LDS budget per workgroup (both ring buffers); PU_LDS_BUDGET_KB overrides (tuning)
+    size_t budget = kLdsBudget;
+    if (const char *env = getenv("PU_LDS_BUDGET_KB")) budget = (size_t)std::max(8, atoi(env)) * 1024;
+    p->ncc = (int)std::max<int64_t>(1, std::min<int64_t>(nchan, (int64_t)(budget / nbuf / chan_bytes)));
     p->lds_bytes = nbuf * (size_t)p->ncc * chan_bytes;
 
     // ---- window records: per (tile, channel, wave) 8 x u16 = LDS byte offset of each

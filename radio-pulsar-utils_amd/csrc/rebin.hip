@@ -4,6 +4,8 @@
 //   pu_rebin_chan   <- quick_chan_rebin         :15-35
 //   pu_roll_rows    <- apply_dm_shifts_to_data  :254-258
 //   pu_roll_and_sum <- roll_and_sum             :60-83
+//   pu_transpose    <- the (nsamps, nchans) -> (nchans, nsamps) transpose sigpyproc's
+//                      readBlock performs (clean.py:327, stats.py:45)
 // Each output element is produced by one lane in the reference's add order, so
 // results are bit-identical to the reference for every supported dtype.
 #include <hip/hip_runtime.h>
@@ -64,9 +66,49 @@ __global__ void roll_and_sum_kernel(const Tin *__restrict__ x, int64_t n, int64_
     sum[t] += static_cast<double>(x[idx]);
 }
 
+// 64x64 tiles through LDS (+1 element pad against bank conflicts); coalesced reads of
+// ``src`` rows and coalesced writes of ``dst`` rows.
+template <typename T>
+__global__ void __launch_bounds__(256) transpose_kernel(const T *__restrict__ src, int64_t rows, int64_t cols,
+                                                        int64_t ld_src, T *__restrict__ dst, int64_t ld_dst)
+{
+    __shared__ T tile[64][65];
+    const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int i = ty; i < 64; i += 4) {
+        const int64_t r = r0 + i, c = c0 + tx;
+        if (r < rows && c < cols) tile[i][tx] = src[r * ld_src + c];
+    }
+    __syncthreads();
+    for (int i = ty; i < 64; i += 4) {
+        const int64_t c = c0 + i, r = r0 + tx;
+        if (r < rows && c < cols) dst[c * ld_dst + r] = tile[tx][i];
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+int pu_transpose(const void *src, int elem_bytes, int64_t rows, int64_t cols, int64_t ld_src, void *dst,
+                 int64_t ld_dst, void *stream)
+{
+    PU_REQUIRE(src && dst && rows >= 0 && cols >= 0 && ld_src >= cols && ld_dst >= rows,
+               "pu_transpose: bad arguments");
+    if (rows == 0 || cols == 0) return PU_OK;
+    PU_REQUIRE((rows + 63) / 64 < 65536, "pu_transpose: too many rows");
+    const dim3 g((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64)), b(256);
+    hipStream_t s = pu::as_stream(stream);
+    switch (elem_bytes) {
+    case 1: hipLaunchKernelGGL(transpose_kernel<uint8_t>, g, b, 0, s, (const uint8_t *)src, rows, cols, ld_src, (uint8_t *)dst, ld_dst); break;
+    case 2: hipLaunchKernelGGL(transpose_kernel<uint16_t>, g, b, 0, s, (const uint16_t *)src, rows, cols, ld_src, (uint16_t *)dst, ld_dst); break;
+    case 4: hipLaunchKernelGGL(transpose_kernel<uint32_t>, g, b, 0, s, (const uint32_t *)src, rows, cols, ld_src, (uint32_t *)dst, ld_dst); break;
+    case 8: hipLaunchKernelGGL(transpose_kernel<uint64_t>, g, b, 0, s, (const uint64_t *)src, rows, cols, ld_src, (uint64_t *)dst, ld_dst); break;
+    default: pu::set_error("pu_transpose: element size %d unsupported", elem_bytes); return PU_EUNSUPPORTED;
+    }
+    return pu::launch_check("transpose_kernel");
+}
+
 
 int pu_rebin_time(const void *x, int dtype, int64_t nrows, int64_t n, int64_t ld, int64_t w, double *out,
                   void *stream)

@@ -46,6 +46,7 @@ SIGNATURES = {
     "pu_rebin_chan": (_i32, [_vp, _i32, _i64, _i64, _i64, _i64, _vp, _vp]),
     "pu_roll_rows": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp]),
     "pu_roll_and_sum": (_i32, [_vp, _i32, _i64, _i64, _vp, _vp]),
+    "pu_transpose": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _i64, _vp]),
 }
 
 INFO_FIELDS = ("ndm", "dm_tiles", "time_tiles", "trials_per_tile", "time_tile", "chans_per_step",

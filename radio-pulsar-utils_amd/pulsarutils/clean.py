@@ -61,7 +61,7 @@ class PulseInfo():
 def _row_sums(x, mode, center=None, scale=None, divisor=0.0):
     t = _hip.torch()
     code = _hip.dtype_code(x.dtype)
-    acc_f32 = code == _hip.PU_F32 and mode != 2
+    acc_f32 = code == _hip.PU_F32 and mode in (0, 1)
     nrows, n = x.shape
     out = t.empty(nrows, dtype=t.float32 if acc_f32 else t.float64, device=x.device)
     ws = t.empty(max(16, _hip.lib().pu_row_sums_workspace_bytes(nrows, n)), dtype=t.uint8, device=x.device)
@@ -213,6 +213,102 @@ def dm_broadening(dm, freq, df):
     return 8300 * dm * df / freq**3
 
 
-__all__ = ["PulseInfo", "get_noisier_channels", "renormalize_data", "measure_channel_variability",
+def search_by_chunks(fname, chunk_length=None, new_sample_time=None, tmin=0, dmmin=200, dmmax=800, surelybad=[],
+                     save_candidates=True, snr_threshold=6, acc=None):
+    """clean.py:276-351: stream a SIGPROC file through clean + DM search, chunk by chunk.
+
+    Same chunking as the reference: ``step = max(int(chunk_length / tsamp) * 2, 128)``
+    samples (``chunk_length`` defaults to the whole-band delay at ``dmmax``), hop
+    ``step // 2`` (50 % overlap), chunks shorter than ``step // 2`` and chunks before
+    ``tmin`` skipped; channel mask from ``get_bad_chans`` (+ ``surelybad``);
+    ``renormalize_data``; band flipped when ``foff < 0``; resampled by
+    ``N = rint(new_sample_time / tsamp)`` when >= 2; ``dedispersion_search``.  All array
+    work stays in HBM (read_block_device -> renormalize_device -> HIP rebin -> search).
+
+    Returns the list of candidate chunks (max S/N > ``snr_threshold``): dicts with
+    istart, iend, t0, best DM, S/N, rebin and the full table.  With ``save_candidates``
+    each candidate's PulseInfo is pickled to ``{root}_{istart}-{iend}.pkl`` like the
+    reference; the diagnostic plots (``plot_diagnostics``, matplotlib + hendrics H-test)
+    are out of scope and not drawn.
+    """
+    import os
+    import pickle
+    from .dedispersion import _rebin_time_device, delta_delay, search_device
+    from .sigproc import FilReader
+    from .stats import get_bad_chans
+    t = _hip.require_gpu()
+    fname_root = os.path.basename(fname).split('.')[0]
+    mask = get_bad_chans(fname)
+    for bad_chan in surelybad:
+        mask[bad_chan] = True
+    fil = FilReader(fname)
+    header = fil.header
+    nsamples = header['nsamples']
+    sample_time = header['tsamp']
+    start_freq = header['fbottom']
+    stop_freq = header['ftop']
+    bandwidth = header['bandwidth']
+    nchan = header['nchans']
+    foff = header['foff']
+    date = header.get('tstart')
+    delta = delta_delay(dmmax, start_freq, stop_freq)
+    if chunk_length is None:
+        chunk_length = delta
+    step = max(int(chunk_length / sample_time) * 2, 128)
+    dm_dt = dm_broadening(dmmin, start_freq, np.abs(foff))
+    if new_sample_time is None:
+        new_sample_time = max(dm_dt / 10, sample_time)
+    sampl_ratio = new_sample_time / sample_time
+    N = 1
+    if sampl_ratio >= 2:
+        N = int(np.rint(sampl_ratio))
+        new_sample_time = N * sample_time
+    trial_DMs = None
+    plan = None
+    candidates = []
+    for istart in range(0, nsamples, step // 2):
+        chunk_size = min(step, nsamples - istart)
+        t0 = istart * sample_time
+        if t0 < tmin:
+            continue
+        if chunk_size < step // 2:
+            continue
+        iend = istart + chunk_size
+        block = fil.read_block_device(istart, chunk_size)
+        if _hip.dtype_code(block.dtype) is None:
+            block = block.to(t.float64)
+        array, _ = renormalize_device(block, badchans_mask=mask)
+        if foff < 0:
+            array = t.flip(array, dims=(0,)).contiguous()
+        if N > 1:
+            array = _rebin_time_device(array, N)
+        nbin = array.shape[1]
+        if trial_DMs is None or plan is None or plan.nsamples != nbin:
+            trial_DMs = dedispersion_plan(nchan, dmmin, dmmax, start_freq, bandwidth, new_sample_time)
+            plan = None
+        (mx, sd, snr, win), plan = search_device(array, trial_DMs, nchan, start_freq, bandwidth, new_sample_time,
+                                                 acc=acc, plan=plan)
+        snr = _host(snr)
+        table = make_table({'DM': trial_DMs, 'max': _host(mx), 'std': _host(sd), 'snr': snr, 'rebin': _host(win)})
+        if np.any(snr > snr_threshold):
+            best = int(np.argmax(snr))
+            cand = {'istart': istart, 'iend': iend, 't0': t0, 'dm': float(trial_DMs[best]),
+                    'snr': float(snr[best]), 'rebin': int(table['rebin'][best]), 'table': table}
+            candidates.append(cand)
+            if save_candidates:
+                info = PulseInfo()
+                info.allprofs = _host(array)
+                info.start_freq = start_freq
+                info.bandwidth = bandwidth
+                info.nbin = nbin
+                info.nchan = array.shape[0]
+                info.date = date
+                info.pulse_freq = 1 / (info.nbin * new_sample_time)
+                with open(f'{fname_root}_{istart}-{iend}.pkl', 'wb') as fh:
+                    pickle.dump(info, fh)
+    return candidates
+
+
+__all__ = ["search_by_chunks", "PulseInfo", "get_noisier_channels", "renormalize_data", "measure_channel_variability",
            "dedispersion_search", "digitize", "dm_broadening", "renormalize_device",
            "channel_means_device", "channel_variances_device", "make_table"]

@@ -25,6 +25,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(REPO, "radio-pulsar-utils_amd"))
 
 from refload import load_reference  # noqa: E402
@@ -205,6 +206,26 @@ if not have("rebin_in"):
     sh = rng.integers(-2000, 2000, 6).astype(float)
     arrays["roll_shifts"] = sh
     arrays["roll_out"] = D.apply_dm_shifts_to_data(x, sh)
+
+# ---------------------------------------------------------------- file statistics (stats.py:35-90)
+# sigpyproc is absent: the reference's get_spectral_stats/get_bad_chans run with their
+# ``FilReader`` name bound to our SIGPROC reader (header/readBlock surface).  What this
+# pins is the reference's chunked statistics + thresholds; the reader is ours on both sides.
+if not have("fil_u8_badchans"):
+    import tempfile
+    from pulsarutils import sigproc
+    tmpd = tempfile.mkdtemp()
+    from synth_files import write_stats_file
+    for dt in ("u8", "f32"):
+        fname, x = write_stats_file(tmpd, dt)
+        meta[f"fil_{dt}_sha256"] = sha(x)
+        ref.stats.FilReader = sigproc.FilReader
+        mean_spec, std_spec = ref.stats.get_spectral_stats(fname)
+        arrays[f"fil_{dt}_mean"] = mean_spec
+        arrays[f"fil_{dt}_std"] = std_spec
+        arrays[f"fil_{dt}_badchans"] = ref.stats.get_bad_chans(fname)
+        meta[f"fil_{dt}_badchans_txt"] = open(fname + ".badchans").read()
+    log("file statistics goldens")
 
 np.savez_compressed(OUT_NPZ, **arrays)
 json.dump(meta, open(OUT_JSON, "w"), indent=1, sort_keys=True)
