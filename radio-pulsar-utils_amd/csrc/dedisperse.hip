@@ -47,7 +47,6 @@ constexpr int kD = 8;                     // trials per wave
 constexpr int kTPT = kWaves * kD;         // trials per tile
 constexpr int kPartStride = 16;           // doubles per (trial, time tile) partial record
 constexpr size_t kLdsBudget = 64 * 1024;  // per workgroup: 2 workgroups / CU
-constexpr int kMaxR = 4;                  // pair mode: distinct relative shifts per pair and tile
 constexpr int kMaxSpread = 2048;
 
 struct DedispArgs {
@@ -64,11 +63,6 @@ struct DedispArgs {
     void *plane;
     int64_t ld_plane;
     double *partials;
-    // pair mode
-    int32_t raw_stride;   // bytes per staged raw channel row
-    int32_t pair_bytes;   // bytes per pair slot in the pair-row region
-    int32_t nrmax;        // pair rows per slot
-    int32_t npairs;
 };
 
 template <typename T>
@@ -91,7 +85,7 @@ __device__ __forceinline__ T ld_uniform(const T *p)
 }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef int i32x4 __attribute__((ext_vector_type(4)));  // pair metadata {base0, base1, offsets, nr}
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 // In-place K-sample window read: 4 x ds_read_b64 at 512-byte strides + wait.  One asm
 // block that overwrites the window registers, so the register allocator never keeps
@@ -433,52 +427,108 @@ dedisp_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const int32_
 
 
 // ---------------------------------------------------------------------------------
-// Pair mode (float32 accumulation of u8 / f32 / f64 inputs).
+// Group mode (float32 accumulation of u8 / f32 / f64 inputs) -- DESIGN.md §4.2.
 //
-// For adjacent channels (c0, c1) = (2p, 2p+1) and the tile's trials, channel c1's
-// shift relative to c0's, r_d = s_d,c1 - s_d,c0, takes nr <= 4 distinct values
-// (adjacent channels' delays drift apart by ~1/nchan sample per trial).  Each chunk
-// stages the raw channel rows by LDS-DMA, then one combine pass writes, for every
-// distinct r, the pair row P_r[j] = x_c0[b0 + j] + x_c1[b0 + r + j] (two alignment
-// copies); a trial then adds ONE pair row per pair: half the adds, half the windows,
-// half the scalar work of the channel mode, exact shift indexing.  Only the float32
-// summation order changes (x_c0 + x_c1 first); uint8 sums stay exact.
-//
-// Per (tile, pair) metadata int4 {base0, base1 (-1: no partner, odd nchan),
-// packed 8-bit row offsets r_i - rmin, nr}; window records index the pair rows.
+// Channels are taken in groups of G adjacent channels.  For trial d and group g the
+// shifts are s_d,c = b_d,g + v_c with b = the group's first-channel shift and v the
+// relative-shift VECTOR of the group; adjacent plan trials share v (a group's channels
+// drift apart by ~G/nchan sample per trial), so a few distinct vectors serve all trials.
+//   1. build_rows_kernel: for every distinct (group, vector) -- a "row" -- the exact
+//      partial sum  R[i] = sum_{k<G} x[c_k][(lo + i + v_k) mod N]  (modular wrap
+//      materialised, so kernel 2 never wraps).  HBM-streaming.
+//   2. dedisp_group_kernel: the channel-mode kernel over groups: per DM tile and group
+//      the rows its trials use ("slots") are staged in LDS by DMA, and a trial adds ONE
+//      window of its slot per group: out_d[t] = sum_g R_{g,v(d,g)}[t + b_d,g - lo].
+// Same sums as the reference (circular shift-and-sum; u8 exact), G x fewer adds.
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x8 __attribute__((ext_vector_type(8)));
+
+// bytes of one alignment copy of a staged row of ``rowlen`` samples (host and device)
+__host__ __device__ constexpr int group_copy_bytes(int rowlen) { return ((rowlen + 2 + 63) & ~63) * 4; }
+
+struct RowsArgs {
+    const void *data;
+    int64_t ld;
+    const int32_t *meta;   // per row: c0, gsize, lo, v_1 .. v_{G-1}   (stride G + 2)
+    float *rows;
+    int64_t ldr;           // floats per row
+    int32_t n, G, nrows, len;  // len = row samples built per segment
+    int32_t T0, small_n;
+};
+
 template <typename Tin>
-__device__ __forceinline__ float raw_at(const unsigned char *row, int i)
+__global__ void __launch_bounds__(256) build_rows_kernel(RowsArgs a)
 {
-    return static_cast<float>(reinterpret_cast<const Tin *>(row)[i]);
+    const int w = pu::xcd_remap(blockIdx.x, gridDim.x);
+    const int r = w % a.nrows;      // rows of one group are adjacent: same XCD, shared L2 lines
+    const int blk = w / a.nrows;
+    const int32_t *m = a.meta + (size_t)r * (a.G + 2);
+    const int c0 = ld_uniform(m), gs = ld_uniform(m + 1);
+    const int n = a.n;
+    int base = ld_uniform(m + 2) + a.T0;
+    if (base >= n) base -= n;
+    const Tin *x = reinterpret_cast<const Tin *>(a.data) + (size_t)c0 * a.ld;
+    float *out = a.rows + (size_t)r * a.ldr;
+    const int i_end = min(a.len, (blk + 1) * 1024);
+    for (int i = blk * 1024 + threadIdx.x; i < i_end; i += 256) {
+        int pos = base + i;
+        if (a.small_n) {
+            pos %= n;
+        } else {
+            if (pos >= n) pos -= n;
+            if (pos >= n) pos -= n;
+        }
+        float acc = static_cast<float>(x[pos]);
+        for (int k = 1; k < gs; ++k) {
+            int idx = pos + ld_uniform(m + 2 + k);
+            if (idx >= n) idx -= n;
+            acc += static_cast<float>(x[(size_t)k * a.ld + idx]);
+        }
+        out[i] = acc;
+    }
 }
 
-// Byte shift between a uint8 raw row's first sample and the dword-aligned address its
-// contiguous DMA started from (0 for wrapping rows, which are moved byte by byte).
-__device__ __forceinline__ int row_shift(int base, int t0, int n, int raw_elems, int small_n)
+struct GroupArgs {
+    DedispArgs o;          // outputs (plane / partials), n, ndt, ntt
+    const float *rows;
+    int64_t ldr;
+    int32_t ngroups;
+    int32_t tt0;           // first time tile of this segment
+    int32_t T0;            // first sample of this segment (rows' origin)
+    int32_t buf_bytes;     // one ring buffer
+};
+
+// One group's contribution to the wave's D trials; u32 records: LDS byte offset in the
+// ring buffer | reload flag << 31.
+__device__ __forceinline__ void group_trials(float (&acc)[kD][8], double (&w)[4], const u32x8 rec, uint32_t base)
 {
-    int start = base + t0;
-    if (start >= n) start -= n;
-    const int al = start & ~3;
-    return (!small_n && al + raw_elems <= n) ? start - al : 0;
+#pragma unroll
+    for (int d = 0; d < kD; ++d) {
+        if (d > 0) {
+            const uint32_t word = rec[d];
+            if (word & 0x80000000u) read_window(w, base + (word & 0x7fffffffu));
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[d][k] += window_elem<float>(w, k);
+        pin_accumulators(acc[d]);
+    }
 }
 
-template <typename Tin, typename Ta, bool PLANE, bool STATS>
-__global__ void __launch_bounds__(kThreads, min_waves_per_simd<Ta>())
-dedisp_pair_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const int32_t *__restrict__ tile_count,
-                   const int32_t *__restrict__ tile_rowlen, const i32x4 *__restrict__ pmeta,
-                   const u32x4 *__restrict__ rec_tab)
+template <bool PLANE, bool STATS>
+__global__ void __launch_bounds__(kThreads, 5)
+dedisp_group_kernel(GroupArgs a, const int32_t *__restrict__ tile_first, const int32_t *__restrict__ tile_count,
+                    const int32_t *__restrict__ tile_rowlen, const i32x2 *__restrict__ tile_chunks,
+                    const i32x4 *__restrict__ chunks, const i32x2 *__restrict__ slots,
+                    const u32x8 *__restrict__ rec_tab)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    typedef float Tl;
-    constexpr int SZ = (int)sizeof(Tin);
-    constexpr int E = 2;
     constexpr int K = 8;
     constexpr int TT = 64 * K;
     constexpr int D = kD;
-
+    const int ndt = a.o.ndt;
     const int wg = pu::xcd_remap(blockIdx.x, gridDim.x);
-    const int dt = wg % a.ndt;
-    const int tt = wg / a.ndt;
+    const int dt = wg % ndt;
+    const int tt = a.tt0 + wg / ndt;
     const int t0 = tt * TT;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -486,144 +536,74 @@ dedisp_pair_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const i
     const int first = ld_uniform(tile_first + dt);
     const int cnt = ld_uniform(tile_count + dt);
     const int rowlen = ld_uniform(tile_rowlen + dt);
+    const i32x2 tc = ld_uniform(tile_chunks + dt);   // {first chunk, chunk count}
     const int slot0 = wave * D;
     const bool active = slot0 < cnt;
-    const int n = a.n;
-    const int stride = a.row_stride;            // floats per pair-row copy
-    const int raw_stride = a.raw_stride;        // bytes per raw row
-    const int raw_elems = raw_stride / SZ;
-    const int pair_bytes = a.pair_bytes;
-    const int raw_region = a.ncc * 2 * raw_stride;
     const uint32_t smem_addr = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char *)smem;
+    const int cover_bytes = (rowlen * 4 + 255) & ~255;
+    const int copy_bytes = group_copy_bytes(rowlen);  // per tile: slot = 2 alignment copies
+    const int slot_bytes = 2 * copy_bytes;
+    const float *rows = a.rows + (t0 - a.T0);
 
-    Ta acc[D][K];
+    float acc[D][K];
 #pragma unroll
     for (int d = 0; d < D; ++d)
 #pragma unroll
-        for (int k = 0; k < K; ++k) acc[d][k] = Ta(0);
+        for (int k = 0; k < K; ++k) acc[d][k] = 0.0f;
 
-    const i32x4 *pm_tile = pmeta + (size_t)dt * a.npairs;
-    const u32x4 *recs = rec_tab + (size_t)dt * a.npairs * kWaves + wave;
-    const Tin *data = reinterpret_cast<const Tin *>(a.data);
-    const int nchunks = (a.npairs + a.ncc - 1) / a.ncc;
+    const u32x8 *recs = rec_tab + (size_t)dt * a.ngroups * kWaves + wave;
 
-    // ---- raw rows of chunk k by LDS-DMA: row 2*pi + w = channel c0 (w=0) / c1 (w=1)
-    auto issue_dma = [&](int k) {
-        const int p0 = k * a.ncc;
-        const int nc = min(a.ncc, a.npairs - p0);
-        for (int r = wave; r < nc * 2; r += kWaves) {
-            const int pi = r >> 1, w = r & 1;
-            const i32x4 pm = ld_uniform(pm_tile + p0 + pi);
-            const int b = w ? pm.y : pm.x;
-            if (b < 0) continue;
-            const int c = 2 * (p0 + pi) + w;
-            const char *row = reinterpret_cast<const char *>(data + (size_t)c * (size_t)a.ld);
-            int start = b + t0;
-            if (start >= n) start -= n;
-            unsigned char *dst = smem + (pi * 2 + w) * raw_stride;
-            if (SZ == 1) start &= ~3;  // dword-aligned DMA source; combine() adds the 0-3 byte shift
-            if (!a.small_n && start + raw_elems <= n) {
-                const char *src = row + (size_t)start * SZ;
-                int off = 0;
-                for (; off + 1024 <= raw_stride; off += 1024)
-                    __builtin_amdgcn_global_load_lds((const void *)(src + off + 16 * lane),
-                                                     (__attribute__((address_space(3))) void *)(dst + off), 16, 0, 0);
-                for (; off < raw_stride; off += 256)
-                    __builtin_amdgcn_global_load_lds((const void *)(src + off + 4 * lane),
-                                                     (__attribute__((address_space(3))) void *)(dst + off), 4, 0, 0);
-            } else if constexpr (SZ == 1) {
-                start = b + t0;  // wrapping row: unaligned start, byte-wise modular DMA
-                if (start >= n) start -= n;
-                for (int off = 0; off < raw_stride; off += 64) {
-                    int idx = start + off + lane;
-                    idx = a.small_n ? idx % n : (idx >= n ? idx - n : idx);
-                    __builtin_amdgcn_global_load_lds((const void *)(row + idx),
-                                                     (__attribute__((address_space(3))) void *)(dst + off), 1, 0, 0);
-                }
-            } else {
-                for (int off = 0; off < raw_stride; off += 256) {
-                    const int byte = off + 4 * lane;
-                    int idx = start + byte / SZ;
-                    idx = a.small_n ? idx % n : (idx >= n ? idx - n : idx);
-                    __builtin_amdgcn_global_load_lds((const void *)(row + (size_t)idx * SZ + (byte % SZ)),
-                                                     (__attribute__((address_space(3))) void *)(dst + off), 4, 0, 0);
-                }
-            }
+    // ---- LDS-DMA of chunk k's slots into ring buffer b: job j = (slot, copy q)
+    auto issue_dma = [&](int k, int b) {
+        const i32x4 ch = ld_uniform(chunks + tc.x + k);  // {group begin, group end, slot begin, slot end}
+        const int njobs = 2 * (ch.w - ch.z);
+        for (int j = wave; j < njobs; j += kWaves) {
+            const i32x2 sl = ld_uniform(slots + ch.z + (j >> 1));  // {row id, start}
+            const int q = j & 1;
+            const char *src = reinterpret_cast<const char *>(rows + (size_t)sl.x * a.ldr + sl.y + q);
+            unsigned char *dst = smem + b * a.buf_bytes + (j >> 1) * slot_bytes + q * copy_bytes;
+            int off = 0;
+            for (; off + 1024 <= cover_bytes; off += 1024)
+                __builtin_amdgcn_global_load_lds((const void *)(src + off + 16 * lane),
+                                                 (__attribute__((address_space(3))) void *)(dst + off), 16, 0, 0);
+            for (; off < cover_bytes; off += 256)
+                __builtin_amdgcn_global_load_lds((const void *)(src + off + 4 * lane),
+                                                 (__attribute__((address_space(3))) void *)(dst + off), 4, 0, 0);
         }
     };
 
-    // ---- combine pass: pair rows (two aligned copies) from the raw rows, 4 samples
-    // per work item: copy0[j..j+3] = P[j..j+3], copy1[j..j+3] = P[j+1..j+4]
-    // exact division of small non-negative ints by a runtime divisor: x / d ==
-    // umulhi(x, ceil(2^32 / d)) for x * d < 2^32 (here x < 2^16)
-    const int nq = (rowlen + 3) >> 2;
-    const uint32_t magic_nq = 0xffffffffu / (uint32_t)nq + 1u;
-    const uint32_t magic_nr = 0xffffffffu / (uint32_t)a.nrmax + 1u;
-    auto combine = [&](int k) {
-        const int p0 = k * a.ncc;
-        const int nc = min(a.ncc, a.npairs - p0);
-        const int total = nc * a.nrmax * nq;
-        for (int item = tid; item < total; item += kThreads) {
-            const int pr = (int)__umulhi((uint32_t)item, magic_nq);   // pair-row slot
-            const int j = (item - pr * nq) * 4;
-            const int pi = (int)__umulhi((uint32_t)pr, magic_nr);
-            const int ri = pr - pi * a.nrmax;
-            const i32x4 pm = pm_tile[p0 + pi];
-            if (ri >= pm.w) continue;
-            int roff = (pm.z >> (8 * ri)) & 0xff;
-            const unsigned char *raw0 = smem + pi * 2 * raw_stride;
-            const unsigned char *raw1 = raw0 + raw_stride;
-            if constexpr (SZ == 1) {  // undo the DMA's dword alignment of contiguous rows
-                raw0 += row_shift(pm.x, t0, n, raw_elems, a.small_n);
-                if (pm.y >= 0) roff += row_shift(pm.y, t0, n, raw_elems, a.small_n);
-            }
-            float v[5];
-#pragma unroll
-            for (int e = 0; e < 5; ++e) v[e] = raw_at<Tin>(raw0, j + e);
-            if (pm.y >= 0) {
-#pragma unroll
-                for (int e = 0; e < 5; ++e) v[e] += raw_at<Tin>(raw1, j + roff + e);
-            }
-            float *prow = reinterpret_cast<float *>(smem + raw_region + pi * pair_bytes) + ri * 2 * stride + j;
-            *reinterpret_cast<float4 *>(prow) = make_float4(v[0], v[1], v[2], v[3]);
-            *reinterpret_cast<float4 *>(prow + stride) = make_float4(v[1], v[2], v[3], v[4]);
-        }
-    };
-
-    issue_dma(0);
-    for (int k = 0; k < nchunks; ++k) {
-        const int p0 = k * a.ncc;
-        const int nc = min(a.ncc, a.npairs - p0);
-        __syncthreads();  // raw(k) landed; every wave left the pair rows of chunk k-1
-        combine(k);
-        __syncthreads();  // pair rows ready; raw rows free
-        if (k + 1 < nchunks) issue_dma(k + 1);
+    issue_dma(0, 0);
+    for (int k = 0; k < tc.y; ++k) {
+        const int b = k & 1;
+        __syncthreads();  // this wave's DMA landed (vmcnt) and every wave left the other buffer
+        if (k + 1 < tc.y) issue_dma(k + 1, b ^ 1);
         if (!active) continue;
-        const uint32_t rows_lane = smem_addr + (uint32_t)raw_region + 8u * lane;
+        const i32x4 ch = ld_uniform(chunks + tc.x + k);
+        const int g0 = ch.x, ng = ch.y - ch.x;
+        const uint32_t base = smem_addr + (uint32_t)(b * a.buf_bytes) + 8u * lane;
         double w0[4], w1[4];
-        const u32x4 *rc = recs + (size_t)p0 * kWaves;
-        u32x4 rec0 = ld_uniform(rc);
-        u32x4 rec1 = nc > 1 ? ld_uniform(rc + kWaves) : rec0;
-        read_window(w0, rows_lane + (rec0[0] & 0x7fffu));
-        for (int ci = 0; ci < nc; ci += 2) {
-            const uint32_t cb0 = rows_lane + (uint32_t)(ci * pair_bytes);
-            const bool has1 = ci + 1 < nc, has2 = ci + 2 < nc, has3 = ci + 3 < nc;
-            u32x4 rec2 = rec0, rec3 = rec1;
-            if (has2) rec2 = ld_uniform(rc + (size_t)(ci + 2) * kWaves);
-            if (has1) prefetch_window(w1, cb0 + pair_bytes + (rec1[0] & 0x7fffu));
-            channel_trials<Tl, Ta, K>(acc, w0, rec0, cb0);
+        const u32x8 *rc = recs + (size_t)g0 * kWaves;
+        u32x8 rec0 = ld_uniform(rc);
+        u32x8 rec1 = ng > 1 ? ld_uniform(rc + kWaves) : rec0;
+        read_window(w0, base + (rec0[0] & 0x7fffffffu));
+        for (int gi = 0; gi < ng; gi += 2) {
+            const bool has1 = gi + 1 < ng, has2 = gi + 2 < ng, has3 = gi + 3 < ng;
+            u32x8 rec2 = rec0, rec3 = rec1;
+            if (has2) rec2 = ld_uniform(rc + (size_t)(gi + 2) * kWaves);
+            if (has1) prefetch_window(w1, base + (rec1[0] & 0x7fffffffu));
+            group_trials(acc, w0, rec0, base);
             if (!has1) break;
             wait_window(w1);
-            if (has3) rec3 = ld_uniform(rc + (size_t)(ci + 3) * kWaves);
-            if (has2) prefetch_window(w0, cb0 + 2 * pair_bytes + (rec2[0] & 0x7fffu));
-            channel_trials<Tl, Ta, K>(acc, w1, rec1, cb0 + pair_bytes);
+            if (has3) rec3 = ld_uniform(rc + (size_t)(gi + 3) * kWaves);
+            if (has2) prefetch_window(w0, base + (rec2[0] & 0x7fffffffu));
+            group_trials(acc, w1, rec1, base);
             if (has2) wait_window(w0);
             rec0 = rec2;
             rec1 = rec3;
         }
     }
     if (!active) return;
-    write_outputs<Tl, Ta, K, PLANE, STATS>(acc, a, first, slot0, cnt, t0, tt, lane);
+    write_outputs<float, float, K, PLANE, STATS>(acc, a.o, first, slot0, cnt, t0, tt, lane);
 }
 
 // One workgroup per trial: combine the per-time-tile partials in a fixed order
@@ -734,12 +714,17 @@ struct pu_plan {
     size_t lds_bytes = 0;
     int32_t *d_first = nullptr, *d_count = nullptr, *d_rowlen = nullptr, *d_base = nullptr;
     u32x4 *d_rec = nullptr;
-    // pair mode
-    bool pair = false;
-    int npairs = 0, raw_stride = 0, pair_bytes = 0, nrmax = 0;
-    i32x4 *d_pmeta = nullptr;
-    // optional kernel timing: event pairs recorded around each dedispersion launch
-    std::vector<hipEvent_t> ev_start, ev_stop;
+    // group mode (group > 1): rows of exact partial sums, built per time segment
+    int group = 1, ngroups = 0, nrows = 0, nseg = 1, seg_len = 0, row_len = 0, buf_bytes = 0, max_span = 0;
+    int64_t nchunks = 0, nslots = 0;
+    float *d_rows = nullptr;
+    int32_t *d_rowmeta = nullptr;
+    i32x2 *d_tile_chunks = nullptr, *d_slots = nullptr;
+    i32x4 *d_chunks = nullptr;
+    u32x8 *d_rec8 = nullptr;
+    // optional kernel timing: events before the first launch, after the first row
+    // build (single-segment plans) and after the last launch of each dispatch
+    std::vector<hipEvent_t> ev_start, ev_mid, ev_stop;
     int64_t launches = 0;
 };
 
@@ -758,24 +743,6 @@ template <typename Tin, typename Tl, typename Ta>
 int launch_variant(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
 {
     const dim3 grid((unsigned)((int64_t)p->ndt * p->ntt)), block(kThreads);
-    if constexpr (std::is_same<Tl, float>::value && std::is_same<Ta, float>::value) {
-        if (p->pair) {
-            if (plane) {
-                auto kern = dedisp_pair_kernel<Tin, Ta, true, false>;
-                int rc = ensure_lds(kern, p->lds_bytes);
-                if (rc) return rc;
-                hipLaunchKernelGGL(kern, grid, block, p->lds_bytes, s, a, p->d_first, p->d_count, p->d_rowlen,
-                                   p->d_pmeta, p->d_rec);
-            } else {
-                auto kern = dedisp_pair_kernel<Tin, Ta, false, true>;
-                int rc = ensure_lds(kern, p->lds_bytes);
-                if (rc) return rc;
-                hipLaunchKernelGGL(kern, grid, block, p->lds_bytes, s, a, p->d_first, p->d_count, p->d_rowlen,
-                                   p->d_pmeta, p->d_rec);
-            }
-            return pu::launch_check("dedisp_pair_kernel");
-        }
-    }
     if (plane) {
         auto kern = dedisp_kernel<Tin, Tl, Ta, true, false>;
         int rc = ensure_lds(kern, p->lds_bytes);
@@ -806,29 +773,103 @@ int dispatch_variant(const pu_plan *p, const DedispArgs &a, bool plane, hipStrea
     return PU_EINVAL;
 }
 
+template <typename Tin>
+void launch_rows(const pu_plan *p, const RowsArgs &ra, hipStream_t s)
+{
+    const int64_t nblk = (int64_t)((ra.len + 1023) / 1024) * ra.nrows;
+    hipLaunchKernelGGL(build_rows_kernel<Tin>, dim3((unsigned)nblk), dim3(256), 0, s, ra);
+}
+
+// Group mode: per time segment, build the rows then sum them.
+int dispatch_group(pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s, hipEvent_t mid)
+{
+    RowsArgs ra{};
+    ra.data = a.data;
+    ra.ld = a.ld;
+    ra.meta = p->d_rowmeta;
+    ra.rows = p->d_rows;
+    ra.ldr = p->row_len;
+    ra.n = (int32_t)p->n;
+    ra.G = p->group;
+    ra.nrows = p->nrows;
+    ra.len = p->row_len;
+    ra.small_n = p->row_len > p->n ? 1 : 0;
+    GroupArgs ga{};
+    ga.o = a;
+    ga.rows = p->d_rows;
+    ga.ldr = p->row_len;
+    ga.ngroups = p->ngroups;
+    ga.buf_bytes = p->buf_bytes;
+    const int tps = p->seg_len / p->TT;  // time tiles per segment
+    for (int sg = 0; sg < p->nseg; ++sg) {
+        ra.T0 = sg * p->seg_len;
+        switch (p->dtype) {
+        case PU_U8: launch_rows<uint8_t>(p, ra, s); break;
+        case PU_F32: launch_rows<float>(p, ra, s); break;
+        default: launch_rows<double>(p, ra, s); break;
+        }
+        int rc = pu::launch_check("build_rows_kernel");
+        if (rc) return rc;
+        if (mid && sg == 0 && p->nseg == 1) PU_TRY_HIP(hipEventRecord(mid, s));
+        ga.T0 = ra.T0;
+        ga.tt0 = sg * tps;
+        const int ntt_seg = std::min(p->ntt - ga.tt0, tps);
+        const dim3 grid((unsigned)((int64_t)p->ndt * ntt_seg)), block(kThreads);
+        if (plane) {
+            auto kern = dedisp_group_kernel<true, false>;
+            rc = ensure_lds(kern, p->lds_bytes);
+            if (rc) return rc;
+            hipLaunchKernelGGL(kern, grid, block, p->lds_bytes, s, ga, p->d_first, p->d_count, p->d_rowlen,
+                               p->d_tile_chunks, p->d_chunks, p->d_slots, p->d_rec8);
+        } else {
+            auto kern = dedisp_group_kernel<false, true>;
+            rc = ensure_lds(kern, p->lds_bytes);
+            if (rc) return rc;
+            hipLaunchKernelGGL(kern, grid, block, p->lds_bytes, s, ga, p->d_first, p->d_count, p->d_rowlen,
+                               p->d_tile_chunks, p->d_chunks, p->d_slots, p->d_rec8);
+        }
+        rc = pu::launch_check("dedisp_group_kernel");
+        if (rc) return rc;
+    }
+    return PU_OK;
+}
+
 int dispatch(pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
 {
     const size_t nslot = p->ev_start.size();
     const size_t slot = nslot ? (size_t)(p->launches % (int64_t)nslot) : 0;
     if (nslot) PU_TRY_HIP(hipEventRecord(p->ev_start[slot], s));
-    int rc = dispatch_variant(p, a, plane, s);
+    int rc = p->group > 1 ? dispatch_group(p, a, plane, s, nslot ? p->ev_mid[slot] : nullptr)
+                          : dispatch_variant(p, a, plane, s);
     if (rc) return rc;
     if (nslot) PU_TRY_HIP(hipEventRecord(p->ev_stop[slot], s));
     ++p->launches;
     return PU_OK;
 }
 
+void destroy_events(pu_plan *p)
+{
+    for (auto *v : {&p->ev_start, &p->ev_mid, &p->ev_stop}) {
+        for (auto e : *v) (void)hipEventDestroy(e);
+        v->clear();
+    }
+}
+
 void free_plan(pu_plan *p)
 {
     if (!p) return;
-    for (auto e : p->ev_start) (void)hipEventDestroy(e);
-    for (auto e : p->ev_stop) (void)hipEventDestroy(e);
+    destroy_events(p);
     (void)hipFree(p->d_first);
     (void)hipFree(p->d_count);
     (void)hipFree(p->d_rowlen);
     (void)hipFree(p->d_base);
     (void)hipFree(p->d_rec);
-    (void)hipFree(p->d_pmeta);
+    (void)hipFree(p->d_rows);
+    (void)hipFree(p->d_rowmeta);
+    (void)hipFree(p->d_tile_chunks);
+    (void)hipFree(p->d_slots);
+    (void)hipFree(p->d_chunks);
+    (void)hipFree(p->d_rec8);
     delete p;
 }
 
@@ -841,12 +882,367 @@ int upload(T **dst, const std::vector<T> &vec)
     return pu::hip_check(hipMemcpy(*dst, vec.data(), bytes, hipMemcpyHostToDevice), "hipMemcpy(plan)");
 }
 
+// ---- channel mode (every variant): DM tiles of <= kTPT trials with per-channel shift
+// spread <= kMaxSpread; per (tile, channel) the modular row base; u16 window records.
+int plan_channels(pu_plan *p, const int64_t *shifts, size_t budget)
+{
+    const int64_t nchan = p->nchan, n = p->n, ndm = p->ndm;
+    const int esz = kVariants[p->variant].lds_elem;
+    const int E = 8 / esz;
+    std::vector<int32_t> first, count;
+    {
+        std::vector<int64_t> mn((size_t)nchan), mx((size_t)nchan);
+        int64_t i = 0;
+        while (i < ndm) {
+            const int64_t *s0 = shifts + i * nchan;
+            for (int64_t c = 0; c < nchan; ++c) mn[c] = mx[c] = s0[c];
+            int64_t j = i + 1;
+            while (j < ndm && j - i < kTPT) {
+                const int64_t *sj = shifts + j * nchan;
+                bool ok = true;
+                for (int64_t c = 0; c < nchan && ok; ++c)
+                    ok = std::max(mx[c], sj[c]) - std::min(mn[c], sj[c]) <= kMaxSpread;
+                if (!ok) break;
+                for (int64_t c = 0; c < nchan; ++c) {
+                    mn[c] = std::min(mn[c], sj[c]);
+                    mx[c] = std::max(mx[c], sj[c]);
+                }
+                ++j;
+            }
+            first.push_back((int32_t)i);
+            count.push_back((int32_t)(j - i));
+            i = j;
+        }
+    }
+    const int ndt = (int)first.size();
+    std::vector<int32_t> rowlen(ndt), base((size_t)ndt * nchan);
+    std::vector<int32_t> rel((size_t)ndt * nchan * kTPT);  // window shift relative to the row base
+    int max_rowlen = 0, max_spread = 0;
+    for (int t = 0; t < ndt; ++t) {
+        const int64_t i0 = first[t];
+        const int cntt = count[t];
+        int spread = 0;
+        for (int64_t c = 0; c < nchan; ++c) {
+            int64_t m0 = INT64_MAX, m1 = INT64_MIN;
+            for (int d = 0; d < cntt; ++d) {
+                m0 = std::min(m0, shifts[(i0 + d) * nchan + c]);
+                m1 = std::max(m1, shifts[(i0 + d) * nchan + c]);
+            }
+            int64_t b0 = m0 % n;
+            if (b0 < 0) b0 += n;
+            base[(size_t)t * nchan + c] = (int32_t)b0;
+            for (int d = 0; d < kTPT; ++d) {
+                const int dd = d < cntt ? d : cntt - 1;  // padding slots repeat the last trial
+                rel[((size_t)t * nchan + c) * kTPT + d] = (int32_t)((shifts[(i0 + dd) * nchan + c] - m0) % n);
+            }
+            spread = std::max(spread, (int)std::min<int64_t>(m1 - m0, n - 1));
+        }
+        max_spread = std::max(max_spread, spread);
+        rowlen[t] = p->TT + spread;
+        max_rowlen = std::max(max_rowlen, rowlen[t]);
+    }
+    const int epp = 256 / esz;
+    p->row_stride = (max_rowlen + E + epp - 1) / epp * epp;
+    p->small_n = (int64_t)p->row_stride + 2 > n ? 1 : 0;
+    const int nbuf = kVariants[p->variant].dma ? 2 : 1;
+    const int64_t chan_bytes = (int64_t)E * p->row_stride * esz;
+    if (chan_bytes > 32768) {
+        pu::set_error("pu_plan_create: LDS row of %d elements does not fit", p->row_stride);
+        return PU_EUNSUPPORTED;
+    }
+    p->ndt = ndt;
+    p->max_spread = max_spread;
+    p->ncc = (int)std::max<int64_t>(1, std::min<int64_t>(nchan, (int64_t)(budget / (nbuf * chan_bytes))));
+    p->lds_bytes = (size_t)p->ncc * nbuf * chan_bytes;
+    if (p->lds_bytes > 160 * 1024) {
+        pu::set_error("pu_plan_create: LDS row of %d elements does not fit", p->row_stride);
+        return PU_EUNSUPPORTED;
+    }
+    // window records: per (tile, channel, wave) 8 x u16 = LDS byte offset of each
+    // trial's window inside the row slot | (differs from the previous trial) << 15
+    const size_t copy_bytes = (size_t)p->row_stride * esz;
+    std::vector<u32x4> rec((size_t)ndt * nchan * kWaves);
+    for (size_t t = 0; t < (size_t)ndt; ++t)
+        for (int64_t c = 0; c < nchan; ++c)
+            for (int w = 0; w < kWaves; ++w) {
+                const int32_t *rr = rel.data() + (t * nchan + c) * kTPT + w * kD;
+                uint32_t words[kD];
+                uint32_t prev = 0xffffffffu;
+                for (int d = 0; d < kD; ++d) {
+                    const uint32_t s = (uint32_t)rr[d];
+                    const uint32_t off = E == 2 ? (uint32_t)((s & 1u) * copy_bytes + (s & ~1u) * 4u) : s * 8u;
+                    words[d] = off | (off != prev ? 0x8000u : 0u);
+                    prev = off;
+                }
+                u32x4 r;
+                for (int u = 0; u < 4; ++u) r[u] = words[2 * u] | (words[2 * u + 1] << 16);
+                rec[(t * nchan + c) * kWaves + w] = r;
+            }
+    if ((int64_t)p->ndt * p->ntt >= (int64_t(1) << 31)) {
+        pu::set_error("pu_plan_create: grid too large");
+        return PU_EINVAL;
+    }
+    int rc = PU_OK;
+    if (!rc) rc = upload(&p->d_first, first);
+    if (!rc) rc = upload(&p->d_count, count);
+    if (!rc) rc = upload(&p->d_rowlen, rowlen);
+    if (!rc) rc = upload(&p->d_base, base);
+    if (!rc) rc = upload(&p->d_rec, rec);
+    return rc;
+}
+
+// ---- group mode planning (float32 accumulation variants).  Returns PU_EUNSUPPORTED
+// when the trial grid does not suit grouping (the caller then plans channel mode).
+constexpr int kRowSpan = 2048;   // max first-channel shift range served by one row
+
+struct SlotAcc {
+    int32_t row, lo, hi;
+};
+
+int plan_group(pu_plan *p, const int64_t *shifts, int G, size_t budget, size_t mem_cap)
+{
+    const int64_t nchan = p->nchan, n = p->n, ndm = p->ndm;
+    const int TT = p->TT;
+    const int ngroups = (int)((nchan + G - 1) / G);
+    const int buf_bytes = (int)(budget / 2) & ~255;
+    std::vector<int32_t> sn((size_t)(ndm * nchan));
+    for (size_t i = 0; i < sn.size(); ++i) {
+        int64_t v = shifts[i] % n;
+        sn[i] = (int32_t)(v < 0 ? v + n : v);
+    }
+    // ---- rows: distinct relative-shift vectors per group, each split into clusters of
+    // first-channel shifts (circularly) no wider than kRowSpan
+    std::vector<int32_t> rowid((size_t)(ndm * ngroups)), roff((size_t)(ndm * ngroups));
+    std::vector<int32_t> meta;
+    int nrows = 0, max_span = 0;
+    std::vector<int32_t> order((size_t)ndm), bs;
+    for (int g = 0; g < ngroups; ++g) {
+        const int64_t c0 = (int64_t)g * G;
+        const int gs = (int)std::min<int64_t>(G, nchan - c0);
+        auto vec = [&](int64_t d, int k) {
+            int32_t v = sn[d * nchan + c0 + k] - sn[d * nchan + c0];
+            return v < 0 ? v + (int32_t)n : v;
+        };
+        auto base_of = [&](int64_t d) { return sn[d * nchan + c0]; };
+        for (int64_t d = 0; d < ndm; ++d) order[d] = (int32_t)d;
+        std::sort(order.begin(), order.end(), [&](int32_t x, int32_t y) {
+            for (int k = 1; k < gs; ++k) {
+                const int32_t a = vec(x, k), b = vec(y, k);
+                if (a != b) return a < b;
+            }
+            if (base_of(x) != base_of(y)) return base_of(x) < base_of(y);
+            return x < y;
+        });
+        for (int64_t a = 0; a < ndm;) {
+            int64_t b = a + 1;
+            while (b < ndm) {
+                bool same = true;
+                for (int k = 1; k < gs && same; ++k) same = vec(order[a], k) == vec(order[b], k);
+                if (!same) break;
+                ++b;
+            }
+            const int64_t m = b - a;
+            // start after the widest circular gap between consecutive (sorted) bases
+            int64_t start = 0, gap = base_of(order[a]) + n - base_of(order[b - 1]);
+            for (int64_t i = 0; i + 1 < m; ++i) {
+                const int64_t gi = base_of(order[a + i + 1]) - base_of(order[a + i]);
+                if (gi > gap) {
+                    gap = gi;
+                    start = i + 1;
+                }
+            }
+            int32_t lo = 0;
+            bool open = false;
+            for (int64_t i = 0; i < m; ++i) {
+                const int32_t d = order[a + (start + i) % m];
+                const int32_t bd = base_of(d);
+                int64_t rel = open ? (bd - lo + n) % n : 0;
+                if (!open || rel > kRowSpan) {
+                    lo = bd;
+                    rel = 0;
+                    open = true;
+                    meta.push_back((int32_t)c0);
+                    meta.push_back(gs);
+                    meta.push_back(lo);
+                    for (int k = 1; k < G; ++k) meta.push_back(k < gs ? vec(d, k) : 0);
+                    ++nrows;
+                }
+                rowid[(size_t)d * ngroups + g] = nrows - 1;
+                roff[(size_t)d * ngroups + g] = (int32_t)rel;
+                max_span = std::max(max_span, (int)rel);
+            }
+            a = b;
+        }
+    }
+    // ---- DM tiles: <= kTPT consecutive trials; every group's slots (distinct rows of the
+    // tile) must fit one ring buffer at the tile's row length
+    std::vector<int32_t> first, count, rowlen;
+    std::vector<std::vector<SlotAcc>> tslots;  // per tile * ngroups
+    {
+        std::vector<std::vector<SlotAcc>> cur((size_t)ngroups), nxt((size_t)ngroups);
+        int64_t i = 0;
+        while (i < ndm) {
+            int spread = 0;
+            for (int g = 0; g < ngroups; ++g) {
+                const size_t k = (size_t)i * ngroups + g;
+                cur[g].assign(1, SlotAcc{rowid[k], roff[k], roff[k]});
+            }
+            int64_t j = i + 1;
+            while (j < ndm && j - i < kTPT) {
+                int sp = spread;
+                size_t maxslots = 0;
+                for (int g = 0; g < ngroups; ++g) {
+                    const size_t k = (size_t)j * ngroups + g;
+                    nxt[g] = cur[g];
+                    bool found = false;
+                    for (auto &sa : nxt[g])
+                        if (sa.row == rowid[k]) {
+                            sa.lo = std::min(sa.lo, roff[k]);
+                            sa.hi = std::max(sa.hi, roff[k]);
+                            sp = std::max(sp, sa.hi - sa.lo);
+                            found = true;
+                        }
+                    if (!found) nxt[g].push_back(SlotAcc{rowid[k], roff[k], roff[k]});
+                    maxslots = std::max(maxslots, nxt[g].size());
+                }
+                if (sp > kMaxSpread || maxslots * 2 * (size_t)group_copy_bytes(TT + sp) > (size_t)buf_bytes) break;
+                std::swap(cur, nxt);
+                spread = sp;
+                ++j;
+            }
+            size_t maxslots = 0;
+            for (int g = 0; g < ngroups; ++g) maxslots = std::max(maxslots, cur[g].size());
+            if (maxslots * 2 * (size_t)group_copy_bytes(TT + spread) > (size_t)buf_bytes) {
+                pu::set_error("group mode: slots of one trial exceed the LDS buffer");
+                return PU_EUNSUPPORTED;
+            }
+            first.push_back((int32_t)i);
+            count.push_back((int32_t)(j - i));
+            rowlen.push_back(TT + spread);
+            for (int g = 0; g < ngroups; ++g) tslots.push_back(cur[g]);
+            p->max_spread = std::max(p->max_spread, spread);
+            i = j;
+        }
+    }
+    const int ndt = (int)first.size();
+    // ---- chunks (groups whose slots fit one buffer), slots, window records
+    std::vector<i32x2> tile_chunks((size_t)ndt), slots;
+    std::vector<i32x4> chunks;
+    std::vector<u32x8> rec((size_t)ndt * ngroups * kWaves);
+    std::vector<int32_t> slot_in_chunk((size_t)ngroups);
+    for (int t = 0; t < ndt; ++t) {
+        const uint32_t copy_bytes = (uint32_t)group_copy_bytes(rowlen[t]);
+        const int cap = (int)((uint32_t)buf_bytes / (2 * copy_bytes));
+        tile_chunks[t] = i32x2{(int32_t)chunks.size(), 0};
+        int g = 0;
+        while (g < ngroups) {
+            const int s_begin = (int)slots.size();
+            int used = 0, g_end = g;
+            while (g_end < ngroups && used + (int)tslots[(size_t)t * ngroups + g_end].size() <= cap) {
+                slot_in_chunk[g_end] = used;
+                for (const auto &sa : tslots[(size_t)t * ngroups + g_end]) slots.push_back(i32x2{sa.row, sa.lo});
+                used += (int)tslots[(size_t)t * ngroups + g_end].size();
+                ++g_end;
+            }
+            chunks.push_back(i32x4{g, g_end, s_begin, (int32_t)slots.size()});
+            tile_chunks[t][1]++;
+            g = g_end;
+        }
+        for (g = 0; g < ngroups; ++g) {
+            const auto &sl = tslots[(size_t)t * ngroups + g];
+            for (int w = 0; w < kWaves; ++w) {
+                u32x8 r;
+                uint32_t prev = 0xffffffffu;
+                for (int d = 0; d < kD; ++d) {
+                    const int dd = std::min(w * kD + d, count[t] - 1);  // padding repeats the last trial
+                    const size_t k = (size_t)(first[t] + dd) * ngroups + g;
+                    int si = 0;
+                    while (sl[si].row != rowid[k]) ++si;
+                    const uint32_t s = (uint32_t)(roff[k] - sl[si].lo);
+                    const uint32_t off = (uint32_t)(slot_in_chunk[g] + si) * 2u * copy_bytes + (s & 1u) * copy_bytes +
+                                         (s & ~1u) * 4u;
+                    r[d] = off | (off != prev ? 0x80000000u : 0u);
+                    prev = off;
+                }
+                rec[((size_t)t * ngroups + g) * kWaves + w] = r;
+            }
+        }
+    }
+    // ---- time segments: the row buffer holds seg_len samples (+ halo) of every row
+    const int64_t ntt = (n + TT - 1) / TT;
+    const int64_t halo = (int64_t)max_span + p->max_spread + 128;
+    int64_t seg_tiles = ntt;
+    while (seg_tiles > 16 && (int64_t)nrows * (seg_tiles * TT + halo) * 4 > (int64_t)mem_cap)
+        seg_tiles = (seg_tiles + 1) / 2;
+    if ((int64_t)nrows * (seg_tiles * TT + halo) * 4 > (int64_t)mem_cap) {
+        pu::set_error("group mode: %d rows exceed the row-buffer cap", nrows);
+        return PU_EUNSUPPORTED;
+    }
+    p->group = G;
+    p->ngroups = ngroups;
+    p->nrows = nrows;
+    p->max_span = max_span;
+    p->seg_len = (int)(seg_tiles * TT);
+    p->nseg = (int)((ntt + seg_tiles - 1) / seg_tiles);
+    p->row_len = (int)((p->seg_len + halo + 63) / 64 * 64);
+    p->buf_bytes = buf_bytes;
+    p->lds_bytes = 2 * (size_t)buf_bytes;
+    p->ndt = ndt;
+    p->ncc = 0;
+    p->row_stride = group_copy_bytes(*std::max_element(rowlen.begin(), rowlen.end())) / 4;
+    p->nchunks = (int64_t)chunks.size();
+    p->nslots = (int64_t)slots.size();
+    if ((int64_t)p->ndt * p->ntt >= (int64_t(1) << 31) || (int64_t)nrows * ((p->row_len + 1023) / 1024) >= (int64_t(1) << 31)) {
+        pu::set_error("pu_plan_create: grid too large");
+        return PU_EINVAL;
+    }
+    int rc = PU_OK;
+    if (!rc) rc = upload(&p->d_first, first);
+    if (!rc) rc = upload(&p->d_count, count);
+    if (!rc) rc = upload(&p->d_rowlen, rowlen);
+    if (!rc) rc = upload(&p->d_tile_chunks, tile_chunks);
+    if (!rc) rc = upload(&p->d_chunks, chunks);
+    if (!rc) rc = upload(&p->d_slots, slots);
+    if (!rc) rc = upload(&p->d_rec8, rec);
+    if (!rc) rc = upload(&p->d_rowmeta, meta);
+    if (!rc)
+        rc = pu::hip_check(hipMalloc((void **)&p->d_rows, (size_t)nrows * p->row_len * sizeof(float)),
+                           "hipMalloc(group rows)");
+    return rc;
+}
+
+void reset_tables(pu_plan *p)
+{
+    pu_plan keep;
+    keep.dtype = p->dtype;
+    keep.acc = p->acc;
+    keep.variant = p->variant;
+    keep.nchan = p->nchan;
+    keep.n = p->n;
+    keep.ndm = p->ndm;
+    keep.K = p->K;
+    keep.TT = p->TT;
+    keep.ntt = p->ntt;
+    (void)hipFree(p->d_first);
+    (void)hipFree(p->d_count);
+    (void)hipFree(p->d_rowlen);
+    (void)hipFree(p->d_base);
+    (void)hipFree(p->d_rec);
+    (void)hipFree(p->d_rows);
+    (void)hipFree(p->d_rowmeta);
+    (void)hipFree(p->d_tile_chunks);
+    (void)hipFree(p->d_slots);
+    (void)hipFree(p->d_chunks);
+    (void)hipFree(p->d_rec8);
+    *p = keep;
+}
+
 }  // namespace
 
 extern "C" {
 
-int pu_plan_create(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t n, const int64_t *shifts,
-                   int64_t ndm)
+int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t n, const int64_t *shifts,
+                           int64_t ndm, int group)
 {
     PU_REQUIRE(out != nullptr, "pu_plan_create: out is NULL");
     *out = nullptr;
@@ -858,6 +1254,8 @@ int pu_plan_create(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t n, 
                (long long)n);
     PU_REQUIRE(ndm > 0 && ndm < (1 << 30), "pu_plan_create: ndm %lld out of range", (long long)ndm);
     PU_REQUIRE(shifts != nullptr, "pu_plan_create: shifts is NULL");
+    PU_REQUIRE(group == 0 || group == 1 || group == 2 || group == 4 || group == 8 || group == 16,
+               "pu_plan_create: group %d not in {0 (auto), 1, 2, 4, 8, 16}", group);
     if (dtype == PU_U8 && acc != PU_ACC_F64)
         PU_REQUIRE(nchan <= 65793, "pu_plan_create: u8 f32 accumulation exact only for nchan <= 65793");
 
@@ -868,225 +1266,42 @@ int pu_plan_create(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t n, 
     p->nchan = nchan;
     p->n = n;
     p->ndm = ndm;
-    const int esz = kVariants[v].lds_elem;
-    const int E = 8 / esz;
+    const int E = 8 / kVariants[v].lds_elem;
     p->K = E * 4;
     p->TT = 64 * p->K;
+    p->ntt = (int)((n + p->TT - 1) / p->TT);
 
     // LDS budget per workgroup; PU_LDS_BUDGET_KB overrides (tuning)
     size_t budget = kLdsBudget;
     if (const char *env = getenv("PU_LDS_BUDGET_KB")) budget = (size_t)std::max(8, atoi(env)) * 1024;
-    // pair mode for float32 accumulation (channel order is not the reference's there anyway)
-    bool want_pair = !kVariants[v].acc_f64 && nchan >= 2 && !getenv("PU_NO_PAIR");
-    const int npairs = (int)((nchan + 1) / 2);
-
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        const bool pair = want_pair && attempt == 0;
-        // ---- greedy DM tiles: up to kTPT consecutive trials whose per-channel shift
-        // spread stays <= kMaxSpread (pair mode: <= kMaxR distinct relative shifts per
-        // pair with span <= 255)
-        std::vector<int32_t> first, count;
-        {
-            std::vector<int64_t> mn((size_t)nchan), mx((size_t)nchan);
-            std::vector<int64_t> rv((size_t)npairs * kMaxR);
-            std::vector<int> nrv((size_t)npairs);
-            int64_t i = 0;
-            while (i < ndm) {
-                const int64_t *s0 = shifts + i * nchan;
-                for (int64_t c = 0; c < nchan; ++c) mn[c] = mx[c] = s0[c];
-                if (pair)
-                    for (int q = 0; q < npairs; ++q) {
-                        nrv[q] = 1;
-                        rv[(size_t)q * kMaxR] = 2 * q + 1 < nchan ? s0[2 * q + 1] - s0[2 * q] : 0;
-                    }
-                int64_t j = i + 1;
-                while (j < ndm && j - i < kTPT) {
-                    const int64_t *sj = shifts + j * nchan;
-                    bool ok = true;
-                    for (int64_t c = 0; c < nchan && ok; ++c)
-                        ok = std::max(mx[c], sj[c]) - std::min(mn[c], sj[c]) <= kMaxSpread;
-                    if (ok && pair) {
-                        for (int q = 0; q < npairs && ok; ++q) {
-                            if (2 * q + 1 >= nchan) continue;
-                            const int64_t r = sj[2 * q + 1] - sj[2 * q];
-                            const int64_t *rq = rv.data() + (size_t)q * kMaxR;
-                            bool seen = false;
-                            int64_t lo = r, hi = r;
-                            for (int t = 0; t < nrv[q]; ++t) {
-                                seen |= rq[t] == r;
-                                lo = std::min(lo, rq[t]);
-                                hi = std::max(hi, rq[t]);
-                            }
-                            if (!seen && (nrv[q] >= kMaxR || hi - lo > 255)) ok = false;
-                        }
-                    }
-                    if (!ok) break;
-                    for (int64_t c = 0; c < nchan; ++c) {
-                        mn[c] = std::min(mn[c], sj[c]);
-                        mx[c] = std::max(mx[c], sj[c]);
-                    }
-                    if (pair)
-                        for (int q = 0; q < npairs; ++q) {
-                            if (2 * q + 1 >= nchan) continue;
-                            const int64_t r = sj[2 * q + 1] - sj[2 * q];
-                            int64_t *rq = rv.data() + (size_t)q * kMaxR;
-                            bool seen = false;
-                            for (int t = 0; t < nrv[q]; ++t) seen |= rq[t] == r;
-                            if (!seen) rq[nrv[q]++] = r;
-                        }
-                    ++j;
-                }
-                first.push_back((int32_t)i);
-                count.push_back((int32_t)(j - i));
-                i = j;
-            }
-        }
-        const int ndt = (int)first.size();
-        // ---- per-tile rows: channel mode = every channel; pair mode = every pair (c0 rows)
-        const int nrows = pair ? npairs : (int)nchan;
-        std::vector<int32_t> rowlen(ndt), base;
-        std::vector<i32x4> pmeta;
-        std::vector<int32_t> rel((size_t)ndt * nrows * kTPT);     // window shift relative to the row base
-        std::vector<int8_t> rowsel((size_t)ndt * nrows * kTPT, 0); // pair row index
-        int max_rowlen = 0, rspan_max = 0, nrmax = 1, max_spread = 0;
-        for (int t = 0; t < ndt; ++t) {
-            const int64_t i0 = first[t];
-            const int cntt = count[t];
-            int spread = 0;
-            for (int q = 0; q < nrows; ++q) {
-                const int c0 = pair ? 2 * q : q;
-                int64_t m0 = INT64_MAX, m1 = INT64_MIN;
-                for (int d = 0; d < cntt; ++d) {
-                    m0 = std::min(m0, shifts[(i0 + d) * nchan + c0]);
-                    m1 = std::max(m1, shifts[(i0 + d) * nchan + c0]);
-                }
-                int64_t b0 = m0 % n;
-                if (b0 < 0) b0 += n;
-                int64_t R[kMaxR];
-                int nr = 1;
-                R[0] = 0;
-                if (pair && c0 + 1 < nchan) {
-                    nr = 0;
-                    for (int d = 0; d < cntt; ++d) {
-                        const int64_t r = shifts[(i0 + d) * nchan + c0 + 1] - shifts[(i0 + d) * nchan + c0];
-                        bool seen = false;
-                        for (int u = 0; u < nr; ++u) seen |= R[u] == r;
-                        if (!seen) R[nr++] = r;
-                    }
-                    std::sort(R, R + nr);
-                }
-                for (int d = 0; d < kTPT; ++d) {
-                    const int dd = d < cntt ? d : cntt - 1;  // padding slots repeat the last trial
-                    const int64_t sc = shifts[(i0 + dd) * nchan + c0];
-                    rel[((size_t)t * nrows + q) * kTPT + d] = (int32_t)((sc - m0) % n);
-                    if (pair && c0 + 1 < nchan) {
-                        const int64_t r = shifts[(i0 + dd) * nchan + c0 + 1] - sc;
-                        rowsel[((size_t)t * nrows + q) * kTPT + d] = (int8_t)(std::find(R, R + nr, r) - R);
-                    }
-                }
-                spread = std::max(spread, (int)std::min<int64_t>(m1 - m0, n - 1));
-                if (pair) {
-                    int32_t packed = 0;
-                    for (int u = 0; u < nr; ++u) packed |= (int32_t)((R[u] - R[0]) & 0xff) << (8 * u);
-                    int32_t b1 = -1;
-                    if (c0 + 1 < nchan) {
-                        int64_t bb = (m0 + R[0]) % n;
-                        if (bb < 0) bb += n;
-                        b1 = (int32_t)bb;
-                        rspan_max = std::max(rspan_max, (int)(R[nr - 1] - R[0]));
-                    }
-                    pmeta.push_back(i32x4{(int32_t)b0, b1, packed, nr});
-                    nrmax = std::max(nrmax, nr);
-                } else {
-                    base.push_back((int32_t)b0);
-                }
-            }
-            max_spread = std::max(max_spread, spread);
-            rowlen[t] = p->TT + spread;
-            max_rowlen = std::max(max_rowlen, rowlen[t]);
-        }
-        // ---- LDS layout
-        const int epp = 256 / esz;
-        int64_t chan_bytes;
-        size_t per_unit;
-        int nbuf = 1;
-        if (pair) {
-            p->row_stride = (max_rowlen + 4 + 63) / 64 * 64;  // floats per pair-row copy
-            const int in_sz = (int)pu::elem_size(dtype);
-            // raw rows: rowlen + 4 (combine reads 4 past the copy) + r span (+3 alignment slack for u8)
-            p->raw_stride = (int)(((int64_t)(max_rowlen + 4 + rspan_max + (in_sz == 1 ? 3 : 0)) * in_sz + 255) / 256 * 256);
-            p->pair_bytes = nrmax * 2 * p->row_stride * 4;
-            p->small_n = (int64_t)p->raw_stride / in_sz + 2 > n ? 1 : 0;
-            chan_bytes = p->pair_bytes;
-            per_unit = (size_t)p->pair_bytes + 2 * (size_t)p->raw_stride;
-            if (p->pair_bytes >= 32768) continue;  // u16 window records cannot address it
-        } else {
-            p->row_stride = (max_rowlen + E + epp - 1) / epp * epp;
-            p->small_n = (int64_t)p->row_stride + 2 > n ? 1 : 0;
-            nbuf = kVariants[v].dma ? 2 : 1;
-            chan_bytes = (int64_t)E * p->row_stride * esz;
-            per_unit = (size_t)nbuf * chan_bytes;
-            if (2 * (int64_t)p->row_stride * esz > 32768) {
-                free_plan(p);
-                pu::set_error("pu_plan_create: LDS row of %d elements does not fit", p->row_stride);
-                return PU_EUNSUPPORTED;
-            }
-        }
-        p->pair = pair;
-        p->npairs = pair ? npairs : 0;
-        p->nrmax = nrmax;
-        p->ndt = ndt;
-        p->ntt = (int)((n + p->TT - 1) / p->TT);
-        p->max_spread = max_spread;
-        p->ncc = (int)std::max<int64_t>(1, std::min<int64_t>(nrows, (int64_t)(budget / per_unit)));
-        p->lds_bytes = (size_t)p->ncc * per_unit;
-        if (p->lds_bytes > 160 * 1024) {
-            free_plan(p);
-            pu::set_error("pu_plan_create: LDS row of %d elements does not fit", p->row_stride);
-            return PU_EUNSUPPORTED;
-        }
-        // ---- window records: per (tile, row, wave) 8 x u16 = LDS byte offset of each
-        // trial's window inside the row slot | (differs from the previous trial) << 15
-        const size_t copy_bytes = (size_t)p->row_stride * (pair ? 4 : esz);
-        std::vector<u32x4> rec((size_t)ndt * nrows * kWaves);
-        for (size_t t = 0; t < (size_t)ndt; ++t)
-            for (int q = 0; q < nrows; ++q)
-                for (int w = 0; w < kWaves; ++w) {
-                    const int32_t *rr = rel.data() + (t * nrows + q) * kTPT + w * kD;
-                    const int8_t *rs = rowsel.data() + (t * nrows + q) * kTPT + w * kD;
-                    uint32_t words[kD];
-                    uint32_t prev = 0xffffffffu;
-                    for (int d = 0; d < kD; ++d) {
-                        const uint32_t s = (uint32_t)rr[d];
-                        uint32_t off = E == 2 ? (uint32_t)((s & 1u) * copy_bytes + (s & ~1u) * 4u) : s * 8u;
-                        off += (uint32_t)rs[d] * 2u * (uint32_t)copy_bytes;
-                        words[d] = off | (off != prev ? 0x8000u : 0u);
-                        prev = off;
-                    }
-                    u32x4 r;
-                    for (int u = 0; u < 4; ++u) r[u] = words[2 * u] | (words[2 * u + 1] << 16);
-                    rec[(t * nrows + q) * kWaves + w] = r;
-                }
-        if ((int64_t)p->ndt * p->ntt >= (int64_t(1) << 31)) {
-            free_plan(p);
-            pu::set_error("pu_plan_create: grid too large");
-            return PU_EINVAL;
-        }
-        int rc = PU_OK;
-        if (!rc) rc = upload(&p->d_first, first);
-        if (!rc) rc = upload(&p->d_count, count);
-        if (!rc) rc = upload(&p->d_rowlen, rowlen);
-        if (!rc && !pair) rc = upload(&p->d_base, base);
-        if (!rc && pair) rc = upload(&p->d_pmeta, pmeta);
-        if (!rc) rc = upload(&p->d_rec, rec);
-        if (rc) {
-            free_plan(p);
-            return rc;
-        }
-        break;
+    size_t mem_cap = size_t(16) << 30;
+    if (const char *env = getenv("PU_ROWS_MB")) mem_cap = (size_t)std::max(1, atoi(env)) << 20;
+    // group size: explicit, else PU_GROUP, else 4; float32 accumulation only (the
+    // float64 modes keep the reference's sequential channel order)
+    int G = group;
+    if (G == 0) {
+        G = 4;
+        if (const char *env = getenv("PU_GROUP")) G = atoi(env);
+    }
+    if (kVariants[v].acc_f64) G = 1;
+    while (G > 1 && G >= nchan) G >>= 1;
+    int rc = PU_EUNSUPPORTED;
+    for (; G > 1 && rc == PU_EUNSUPPORTED; G >>= 1) {
+        rc = plan_group(p, shifts, G, budget, mem_cap);
+        if (rc == PU_EUNSUPPORTED) reset_tables(p);
+    }
+    if (rc == PU_EUNSUPPORTED) rc = plan_channels(p, shifts, budget);
+    if (rc) {
+        free_plan(p);
+        return rc;
     }
     *out = p;
     return PU_OK;
+}
+
+int pu_plan_create(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t n, const int64_t *shifts, int64_t ndm)
+{
+    return pu_plan_create_grouped(out, dtype, acc, nchan, n, shifts, ndm, 0);
 }
 
 void pu_plan_destroy(pu_plan *p) { free_plan(p); }
@@ -1094,13 +1309,10 @@ void pu_plan_destroy(pu_plan *p) { free_plan(p); }
 int pu_plan_enable_timing(pu_plan *p, int nslots)
 {
     PU_REQUIRE(p != nullptr && nslots >= 0 && nslots <= 65536, "pu_plan_enable_timing: bad arguments");
-    for (auto e : p->ev_start) (void)hipEventDestroy(e);
-    for (auto e : p->ev_stop) (void)hipEventDestroy(e);
-    p->ev_start.assign((size_t)nslots, nullptr);
-    p->ev_stop.assign((size_t)nslots, nullptr);
-    for (int i = 0; i < nslots; ++i) {
-        PU_TRY_HIP(hipEventCreate(&p->ev_start[i]));
-        PU_TRY_HIP(hipEventCreate(&p->ev_stop[i]));
+    destroy_events(p);
+    for (auto *v : {&p->ev_start, &p->ev_mid, &p->ev_stop}) {
+        v->assign((size_t)nslots, nullptr);
+        for (int i = 0; i < nslots; ++i) PU_TRY_HIP(hipEventCreate(&(*v)[i]));
     }
     p->launches = 0;
     return PU_OK;
@@ -1118,6 +1330,20 @@ int pu_plan_kernel_times(pu_plan *p, float *ms, int n)
     return m;
 }
 
+int pu_plan_phase_times(pu_plan *p, float *build_ms, float *sum_ms, int n)
+{
+    PU_REQUIRE(p != nullptr && build_ms != nullptr && sum_ms != nullptr, "pu_plan_phase_times: bad arguments");
+    if (p->group <= 1 || p->nseg != 1) return 0;
+    const int64_t have = std::min<int64_t>(p->launches, (int64_t)p->ev_start.size());
+    const int m = (int)std::min<int64_t>(n, have);
+    for (int i = 0; i < m; ++i) {
+        PU_TRY_HIP(hipEventSynchronize(p->ev_stop[i]));
+        PU_TRY_HIP(hipEventElapsedTime(&build_ms[i], p->ev_start[i], p->ev_mid[i]));
+        PU_TRY_HIP(hipEventElapsedTime(&sum_ms[i], p->ev_mid[i], p->ev_stop[i]));
+    }
+    return m;
+}
+
 size_t pu_plan_workspace_bytes(const pu_plan *p)
 {
     if (!p) return 0;
@@ -1128,7 +1354,8 @@ int pu_plan_info(const pu_plan *p, int64_t *info, int n)
 {
     if (!p || !info) return 0;
     const int64_t v[] = {p->ndm, p->ndt, p->ntt, kTPT, p->TT, p->ncc,
-                         p->row_stride, (int64_t)p->lds_bytes, kVariants[p->variant].acc_f64, p->max_spread};
+                         p->row_stride, (int64_t)p->lds_bytes, kVariants[p->variant].acc_f64, p->max_spread,
+                         p->group, p->nrows, p->nseg, (int64_t)p->nrows * p->row_len * 4, p->nslots};
     const int m = std::min<int>(n, (int)(sizeof v / sizeof v[0]));
     for (int k = 0; k < m; ++k) info[k] = v[k];
     return m;
@@ -1142,13 +1369,8 @@ static int check_data(const pu_plan *p, const void *data, int64_t ld)
     return PU_OK;
 }
 
-int pu_plan_search(pu_plan *p, const void *data, int64_t ld, double *max_out, double *std_out,
-                   double *snr_out, int32_t *rebin_out, void *workspace, size_t ws_bytes, void *stream)
+static DedispArgs make_args(const pu_plan *p, const void *data, int64_t ld)
 {
-    int rc = check_data(p, data, ld);
-    if (rc) return rc;
-    PU_REQUIRE(max_out && std_out && snr_out && rebin_out, "pu_plan_search: NULL output");
-    PU_REQUIRE(workspace && ws_bytes >= pu_plan_workspace_bytes(p), "pu_plan_search: workspace too small");
     DedispArgs a{};
     a.data = data;
     a.ld = ld;
@@ -1159,10 +1381,17 @@ int pu_plan_search(pu_plan *p, const void *data, int64_t ld, double *max_out, do
     a.ncc = p->ncc;
     a.row_stride = p->row_stride;
     a.small_n = p->small_n;
-    a.raw_stride = p->raw_stride;
-    a.pair_bytes = p->pair_bytes;
-    a.nrmax = p->nrmax;
-    a.npairs = p->npairs;
+    return a;
+}
+
+int pu_plan_search(pu_plan *p, const void *data, int64_t ld, double *max_out, double *std_out,
+                   double *snr_out, int32_t *rebin_out, void *workspace, size_t ws_bytes, void *stream)
+{
+    int rc = check_data(p, data, ld);
+    if (rc) return rc;
+    PU_REQUIRE(max_out && std_out && snr_out && rebin_out, "pu_plan_search: NULL output");
+    PU_REQUIRE(workspace && ws_bytes >= pu_plan_workspace_bytes(p), "pu_plan_search: workspace too small");
+    DedispArgs a = make_args(p, data, ld);
     a.partials = reinterpret_cast<double *>(workspace);
     hipStream_t s = pu::as_stream(stream);
     rc = dispatch(p, a, false, s);
@@ -1178,20 +1407,7 @@ int pu_plan_dedisperse(pu_plan *p, const void *data, int64_t ld, void *plane, in
     if (rc) return rc;
     PU_REQUIRE(plane != nullptr, "pu_plan_dedisperse: plane is NULL");
     PU_REQUIRE(ld_plane >= p->n, "pu_plan_dedisperse: ld_plane < nsamples");
-    DedispArgs a{};
-    a.data = data;
-    a.ld = ld;
-    a.nchan = (int32_t)p->nchan;
-    a.n = (int32_t)p->n;
-    a.ndt = p->ndt;
-    a.ntt = p->ntt;
-    a.ncc = p->ncc;
-    a.row_stride = p->row_stride;
-    a.small_n = p->small_n;
-    a.raw_stride = p->raw_stride;
-    a.pair_bytes = p->pair_bytes;
-    a.nrmax = p->nrmax;
-    a.npairs = p->npairs;
+    DedispArgs a = make_args(p, data, ld);
     a.plane = plane;
     a.ld_plane = ld_plane;
     return dispatch(p, a, true, pu::as_stream(stream));

@@ -28,6 +28,7 @@ SIGNATURES = {
     "pu_last_error": (ctypes.c_char_p, []),
     "pu_shift_table": (_i32, [_i64, _vp, _i64, _f64, _f64, _f64, _vp]),
     "pu_plan_create": (_i32, [ctypes.POINTER(_vp), _i32, _i32, _i64, _i64, _vp, _i64]),
+    "pu_plan_create_grouped": (_i32, [ctypes.POINTER(_vp), _i32, _i32, _i64, _i64, _vp, _i64, _i32]),
     "pu_plan_destroy": (None, [_vp]),
     "pu_plan_workspace_bytes": (_sz, [_vp]),
     "pu_plan_search": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
@@ -35,6 +36,7 @@ SIGNATURES = {
     "pu_plan_info": (_i32, [_vp, _vp, _i32]),
     "pu_plan_enable_timing": (_i32, [_vp, _i32]),
     "pu_plan_kernel_times": (_i32, [_vp, _vp, _i32]),
+    "pu_plan_phase_times": (_i32, [_vp, _vp, _vp, _i32]),
     "pu_row_sums": (_i32, [_vp, _i32, _i64, _i64, _i64, _i32, _vp, _vp, _f64, _vp, _vp, _sz, _vp]),
     "pu_row_sums_workspace_bytes": (_sz, [_i64, _i64]),
     "pu_col_means": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp]),
@@ -50,7 +52,8 @@ SIGNATURES = {
 }
 
 INFO_FIELDS = ("ndm", "dm_tiles", "time_tiles", "trials_per_tile", "time_tile", "chans_per_step",
-               "row_stride", "lds_bytes", "acc_is_f64", "max_spread")
+               "row_stride", "lds_bytes", "acc_is_f64", "max_spread", "group", "group_rows", "segments",
+               "row_buffer_bytes", "slots")
 
 
 class HipBackendError(RuntimeError):
@@ -147,14 +150,17 @@ def to_device(a, allowed=(PU_U8, PU_F32, PU_F64), device=None):
 class Plan:
     """Owning wrapper of a ``pu_plan`` (dedispersion tiling + device metadata)."""
 
-    def __init__(self, dtype_code_, acc, nchan, nsamples, shifts):
+    def __init__(self, dtype_code_, acc, nchan, nsamples, shifts, group=0):
+        """``group``: channels summed per group row (0 = library default, 1 = channel
+        mode, 2/4/8/16); float64 accumulation always uses channel mode."""
         require_gpu()
         sh = np.ascontiguousarray(shifts, dtype=np.int64)
         ndm = sh.shape[0]
         assert sh.shape == (ndm, nchan)
         h = ctypes.c_void_p()
-        check(lib().pu_plan_create(ctypes.byref(h), dtype_code_, acc, nchan, nsamples,
-                                   sh.ctypes.data_as(ctypes.c_void_p), ndm), "pu_plan_create")
+        check(lib().pu_plan_create_grouped(ctypes.byref(h), dtype_code_, acc, nchan, nsamples,
+                                           sh.ctypes.data_as(ctypes.c_void_p), ndm, int(group)),
+              "pu_plan_create")
         self._h = h
         self.dtype_code = dtype_code_
         self.nchan, self.nsamples, self.ndm = nchan, nsamples, ndm
@@ -202,6 +208,16 @@ class Plan:
         if m < 0:
             check(m, "pu_plan_kernel_times")
         return out[:m]
+
+    def phase_times_ms(self, n):
+        """(row-build ms, group-sum ms) per timed launch (single-segment group plans)."""
+        b = np.zeros(int(n), np.float32)
+        g = np.zeros(int(n), np.float32)
+        m = lib().pu_plan_phase_times(self._h, b.ctypes.data_as(ctypes.c_void_p), g.ctypes.data_as(ctypes.c_void_p),
+                                      int(n))
+        if m < 0:
+            check(m, "pu_plan_phase_times")
+        return b[:m], g[:m]
 
     def dedisperse(self, data, plane=None, stream=None):
         """Dedispersed plane (ndm, nsamples) in the accumulation dtype."""

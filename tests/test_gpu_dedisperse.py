@@ -102,15 +102,19 @@ def test_dedisperse_random_shapes_exact_f64(gpu, dt, shape):
     np.testing.assert_array_equal(D.dedisperse(x, sh), oracle.dedisperse(x, sh.astype(np.int64)))
 
 
-def _plane(x, shifts, acc):
+def _plane(x, shifts, acc, group=0, info=None):
     t = _hip.require_gpu()
     xd = _hip.to_device(x)
-    plan = _hip.Plan(_hip.dtype_code(xd.dtype), D._acc_code(acc), x.shape[0], x.shape[1], shifts)
+    plan = _hip.Plan(_hip.dtype_code(xd.dtype), D._acc_code(acc), x.shape[0], x.shape[1], shifts, group=group)
+    if info is not None:
+        info.update(plan.info)
     return plan.dedisperse(xd).cpu().numpy()
 
 
+@pytest.mark.parametrize("group", [1, 2, 4, 8])
 @pytest.mark.parametrize("name", ["C1", "C5"])
-def test_plane_native_vs_oracle(gpu, golden, name):
+def test_plane_native_vs_oracle(gpu, golden, name, group):
+    """float32 accumulation, channel mode (group 1) and group mode (exact group rows)."""
     arrays, _ = golden
     c = CONFIGS[name]
     rng = np.random.default_rng(11)
@@ -119,13 +123,15 @@ def test_plane_native_vs_oracle(gpu, golden, name):
     dms = arrays[f"plan_{name}"]
     idx = np.linspace(0, dms.size - 1, 40).astype(int)
     sh = _hip.shift_table(c.nchan, dms[idx], c.start_freq, c.bandwidth, c.tsamp)
-    plane = _plane(x, sh, "native")
+    info = {}
+    plane = _plane(x, sh, "native", group, info)
     assert plane.dtype == np.float32
+    assert info["group"] == group or (group > 1 and info["group"] < group), info
     for k in range(len(idx)):
         ref = oracle.dedisperse(x, sh[k])
         assert np.all(np.abs(plane[k] - ref) <= f32_bound(x, sh[k])), k
     u = (x * 100).astype(np.uint8)
-    pu = _plane(u, sh, "native")
+    pu = _plane(u, sh, "native", group)
     for k in range(0, len(idx), 5):
         np.testing.assert_array_equal(pu[k].astype(np.float64), oracle.dedisperse(u, sh[k]))
     p64 = _plane(x, sh, "f64")
@@ -142,6 +148,33 @@ def test_plane_arbitrary_dm_list_large_spread(gpu):
     plane = _plane(x, sh, "f64")
     for k in range(70):
         np.testing.assert_array_equal(plane[k], oracle.dedisperse(x, sh[k]))
+    u = (np.abs(x) * 40).astype(np.uint8)
+    for group in (1, 4):
+        pu = _plane(u, sh, "native", group)
+        for k in range(70):
+            np.testing.assert_array_equal(pu[k].astype(np.float64), oracle.dedisperse(u, sh[k]))
+
+
+@pytest.mark.parametrize("dt", ["u8", "f32"])
+def test_plane_group_mode_segmented(gpu, dt, monkeypatch):
+    """A row-buffer cap that forces several time segments (build + sum per segment)."""
+    c = CONFIGS["C5"]
+    rng = np.random.default_rng(21)
+    n = 1 << 16
+    x = rng.random((c.nchan, n)) * 50
+    x = x.astype(np.uint8) if dt == "u8" else x.astype(np.float32)
+    dms = np.linspace(c.dmmin, c.dmmax, 90)
+    sh = _hip.shift_table(c.nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
+    monkeypatch.setenv("PU_ROWS_MB", "24")
+    info = {}
+    plane = _plane(x, sh, "native", 4, info)
+    assert info["group"] == 4 and info["segments"] > 1, info
+    for k in range(0, 90, 7):
+        ref = oracle.dedisperse(x, sh[k])
+        if dt == "u8":
+            np.testing.assert_array_equal(plane[k].astype(np.float64), ref)
+        else:
+            assert np.all(np.abs(plane[k] - ref) <= f32_bound(x, sh[k])), k
 
 
 # ------------------------------------------------------------------ search tables
@@ -197,9 +230,11 @@ def test_search_c1_float32_accumulation(gpu, golden, acc):
     np.testing.assert_allclose(sd, arrays["c1_table_std"], rtol=tol)
 
 
+@pytest.mark.parametrize("group", ["1", "4"])
 @pytest.mark.parametrize("dt", ["f32", "u8"])
-def test_search_ragged_small(gpu, dt):
+def test_search_ragged_small(gpu, dt, group, monkeypatch):
     """Tiny / ragged inputs: N smaller than a time tile, odd nchan, N % 8 != 0."""
+    monkeypatch.setenv("PU_GROUP", group)
     rng = np.random.default_rng(3)
     for nchan, n in [(3, 37), (5, 200), (31, 1001), (130, 3000)]:
         x = rng.random((nchan, n)) * 10
