@@ -71,7 +71,7 @@ int pu_plan_create(pu_plan **plan, int dtype, int acc, int64_t nchan, int64_t ns
 /* Same, choosing the float32-accumulation strategy: ``group`` = channels summed into
  * one exact partial-sum row per distinct relative-shift vector:
  * 0 = default (PU_GROUP env or 4, falling back to smaller groups / channel mode when
- * the trial grid does not suit it), 1 = channel mode, 2/4/8/16.  Float64
+ * the trial grid does not suit it), 1 = channel mode, 2/4/8.  Float64
  * accumulation always runs channel mode (the reference's channel order). */
 int pu_plan_create_grouped(pu_plan **plan, int dtype, int acc, int64_t nchan, int64_t nsamples,
                            const int64_t *shifts, int64_t ndm, int group);
@@ -100,14 +100,11 @@ int pu_plan_enable_timing(pu_plan *plan, int nslots);
 /* Synchronises on the recorded events and writes up to ``n`` kernel durations (ms,
  * launch order).  Returns the number written, or a negative PU_E* code. */
 int pu_plan_kernel_times(pu_plan *plan, float *ms, int n);
-/* Group-mode plans with one time segment: the same launches split into the row build
- * and the group sum (ms each).  Returns the count written (0 for other plans). */
-int pu_plan_phase_times(pu_plan *plan, float *build_ms, float *sum_ms, int n);
 
 /* Introspection (tests / DESIGN.md): fills up to ``n`` of
  * {ndm, dm_tiles, time_tiles, trials_per_tile, time_tile, chans_per_step,
- *  row_stride, lds_bytes, acc_is_f64, max_spread, group, group_rows, segments,
- *  row_buffer_bytes, slots}. Returns the count written. */
+ *  row_stride, lds_bytes, acc_is_f64, max_spread, group, slots, stages,
+ *  slot_area, raw_stride}. Returns the count written. */
 int pu_plan_info(const pu_plan *plan, int64_t *info, int n);
 
 /* ------------------------------------------------------------------ cleaning */

@@ -41,7 +41,7 @@
 
 namespace {
 
-constexpr int kWaves = 10;                // waves per workgroup (each owns D trials): 2 WGs = 5 waves/SIMD
+constexpr int kWaves = 8;                 // waves per workgroup (each owns D trials): 2 WGs = 4 waves/SIMD
 constexpr int kThreads = kWaves * 64;
 constexpr int kD = 8;                     // trials per wave
 constexpr int kTPT = kWaves * kD;         // trials per tile
@@ -260,13 +260,8 @@ __device__ __forceinline__ void write_outputs(const Ta (&acc)[kD][K], const Dedi
     }
 }
 
-// float32 accumulators: 2 workgroups x 10 waves per CU = 5 waves per SIMD (<= 96 VGPRs);
-// float64 accumulators (reference-exact mode, 128 accumulator VGPRs): 1 workgroup.
-template <typename Ta>
-constexpr int min_waves_per_simd() { return sizeof(Ta) == 8 ? 3 : 5; }
-
 template <typename Tin, typename Tl, typename Ta, bool PLANE, bool STATS>
-__global__ void __launch_bounds__(kThreads, min_waves_per_simd<Ta>())
+__global__ void __launch_bounds__(kThreads)
 dedisp_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const int32_t *__restrict__ tile_count,
               const int32_t *__restrict__ tile_rowlen, const int32_t *__restrict__ base_tab,
               const u32x4 *__restrict__ rec_tab)
@@ -427,123 +422,149 @@ dedisp_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const int32_
 
 
 // ---------------------------------------------------------------------------------
-// Group mode (float32 accumulation of u8 / f32 / f64 inputs) -- DESIGN.md §4.2.
+// Subband mode (float32 accumulation of u8 / f32 / f64 inputs) -- DESIGN.md §4.2.
 //
 // Channels are taken in groups of G adjacent channels.  For trial d and group g the
-// shifts are s_d,c = b_d,g + v_c with b = the group's first-channel shift and v the
-// relative-shift VECTOR of the group; adjacent plan trials share v (a group's channels
-// drift apart by ~G/nchan sample per trial), so a few distinct vectors serve all trials.
-//   1. build_rows_kernel: for every distinct (group, vector) -- a "row" -- the exact
-//      partial sum  R[i] = sum_{k<G} x[c_k][(lo + i + v_k) mod N]  (modular wrap
-//      materialised, so kernel 2 never wraps).  HBM-streaming.
-//   2. dedisp_group_kernel: the channel-mode kernel over groups: per DM tile and group
-//      the rows its trials use ("slots") are staged in LDS by DMA, and a trial adds ONE
-//      window of its slot per group: out_d[t] = sum_g R_{g,v(d,g)}[t + b_d,g - lo].
-// Same sums as the reference (circular shift-and-sum; u8 exact), G x fewer adds.
+// shifts are s_{d,c0+k} = b_d + v_k, with b_d the group's first-channel shift and v the
+// group's relative-shift VECTOR.  Adjacent plan trials share v (a group's channels drift
+// apart by ~G/nchan sample per trial), so the 64 trials of a DM tile need one or two
+// distinct vectors per group.  Per (DM tile, time tile) workgroup, stage by stage (a
+// stage = a few consecutive groups):
+//   1. build: for every distinct vector v of the tile in the stage's groups -- a "slot"
+//      -- the exact partial sum  R[i] = sum_{k<G} x[c0+k][(t0 + lo + v_k + i) mod N]
+//      into LDS (two alignment copies: R[i] and R[i+1] at the same offset), from the
+//      stage's channel rows staged in LDS by DMA (f32) or straight from global memory
+//      (u8 / f64, converted to f32);
+//   2. sum: every trial adds ONE window of its slot per group:
+//      out_d[t0 + i] += R_{v(d)}[i + b_d - lo].
+// The gathered elements are the reference's (circular shift-and-sum; u8 exact), with
+// G x fewer adds than channel mode and each channel row read from L2 once per tile.
 typedef int i32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x8 __attribute__((ext_vector_type(8)));
 
-// bytes of one alignment copy of a staged row of ``rowlen`` samples (host and device)
-__host__ __device__ constexpr int group_copy_bytes(int rowlen) { return ((rowlen + 2 + 63) & ~63) * 4; }
+constexpr int kSWaves = 8;                // subband mode: waves per workgroup (2 WGs = 4 waves/SIMD)
+constexpr int kSThreads = kSWaves * 64;
+constexpr int kSTPT = kSWaves * kD;       // trials per tile
+constexpr size_t kSubLdsBudget = 80 * 1024;
 
-struct RowsArgs {
-    const void *data;
-    int64_t ld;
-    const int32_t *meta;   // per row: c0, gsize, lo, v_1 .. v_{G-1}   (stride G + 2)
-    float *rows;
-    int64_t ldr;           // floats per row
-    int32_t n, G, nrows, len;  // len = row samples built per segment
-    int32_t T0, small_n;
+struct SubArgs {
+    DedispArgs o;           // data, ld, nchan, n, ndt, ntt, small_n; plane / partials
+    int32_t ngroups;
+    int32_t raw_stride;     // floats per staged channel row (DMA mode)
+    int32_t slot_area;      // LDS byte offset of the slot area
 };
 
-template <typename Tin>
-__global__ void __launch_bounds__(256) build_rows_kernel(RowsArgs a)
+// Counted LDS wait that also "defines" the window registers it guards, so the adds
+// that read them cannot be hoisted above it.  lgkmcnt counts the inline-asm reads in
+// issue order; an outstanding scalar load only makes the wait longer, never shorter.
+template <int N>
+__device__ __forceinline__ void wait_lgkm(double (&w)[4])
 {
-    const int w = pu::xcd_remap(blockIdx.x, gridDim.x);
-    const int r = w % a.nrows;      // rows of one group are adjacent: same XCD, shared L2 lines
-    const int blk = w / a.nrows;
-    const int32_t *m = a.meta + (size_t)r * (a.G + 2);
-    const int c0 = ld_uniform(m), gs = ld_uniform(m + 1);
-    const int n = a.n;
-    int base = ld_uniform(m + 2) + a.T0;
-    if (base >= n) base -= n;
-    const Tin *x = reinterpret_cast<const Tin *>(a.data) + (size_t)c0 * a.ld;
-    float *out = a.rows + (size_t)r * a.ldr;
-    const int i_end = min(a.len, (blk + 1) * 1024);
-    for (int i = blk * 1024 + threadIdx.x; i < i_end; i += 256) {
-        int pos = base + i;
-        if (a.small_n) {
-            pos %= n;
-        } else {
-            if (pos >= n) pos -= n;
-            if (pos >= n) pos -= n;
-        }
-        float acc = static_cast<float>(x[pos]);
-        for (int k = 1; k < gs; ++k) {
-            int idx = pos + ld_uniform(m + 2 + k);
-            if (idx >= n) idx -= n;
-            acc += static_cast<float>(x[(size_t)k * a.ld + idx]);
-        }
-        out[i] = acc;
-    }
+    static_assert(N == 0 || N == 4 || N == 8 || N == 12, "lgkmcnt");
+    if constexpr (N == 12)
+        asm volatile("s_waitcnt lgkmcnt(12)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]) : : "memory");
+    else if constexpr (N == 8)
+        asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]) : : "memory");
+    else if constexpr (N == 4)
+        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]) : : "memory");
+    else
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]) : : "memory");
 }
 
-struct GroupArgs {
-    DedispArgs o;          // outputs (plane / partials), n, ndt, ntt
-    const float *rows;
-    int64_t ldr;
-    int32_t ngroups;
-    int32_t tt0;           // first time tile of this segment
-    int32_t T0;            // first sample of this segment (rows' origin)
-    int32_t buf_bytes;     // one ring buffer
-};
-
-// One group's contribution to the wave's D trials; u32 records: LDS byte offset in the
-// ring buffer | reload flag << 31.
-__device__ __forceinline__ void group_trials(float (&acc)[kD][8], double (&w)[4], const u32x8 rec, uint32_t base)
+// One group's contribution to the wave's D trials: rec[d] = LDS byte offset (slot area
+// relative) of trial d's window.  Every trial reads its window (4 x ds_read_b64 in
+// inline asm: hipcc would merge them into ds_read2st64_b64, half the LDS rate), three
+// trials ahead of the adds, with counted waits.
+__device__ __forceinline__ void group_trials(float (&acc)[kD][8], const u32x8 rec, uint32_t base)
 {
+    double w[4][4];
+    prefetch_window(w[0], base + rec[0]);
+    prefetch_window(w[1], base + rec[1]);
+    prefetch_window(w[2], base + rec[2]);
 #pragma unroll
     for (int d = 0; d < kD; ++d) {
-        if (d > 0) {
-            const uint32_t word = rec[d];
-            if (word & 0x80000000u) read_window(w, base + (word & 0x7fffffffu));
+        if (d + 3 < kD) prefetch_window(w[(d + 3) & 3], base + rec[d + 3]);
+        constexpr int kAhead[kD] = {3, 3, 3, 3, 3, 2, 1, 0};
+        double(&wd)[4] = w[d & 3];
+        switch (kAhead[d]) {
+        case 3: wait_lgkm<12>(wd); break;
+        case 2: wait_lgkm<8>(wd); break;
+        case 1: wait_lgkm<4>(wd); break;
+        default: wait_lgkm<0>(wd); break;
         }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc[d][k] += window_elem<float>(w, k);
+        for (int k = 0; k < 8; ++k) acc[d][k] += window_elem<float>(wd, k);
         pin_accumulators(acc[d]);
     }
 }
 
-template <bool PLANE, bool STATS>
-__global__ void __launch_bounds__(kThreads, 5)
-dedisp_group_kernel(GroupArgs a, const int32_t *__restrict__ tile_first, const int32_t *__restrict__ tile_count,
-                    const int32_t *__restrict__ tile_rowlen, const i32x2 *__restrict__ tile_chunks,
-                    const i32x4 *__restrict__ chunks, const i32x2 *__restrict__ slots,
-                    const u32x8 *__restrict__ rec_tab)
+// LDS-DMA of one channel-row window [start, start + cover) mod n (float32) into dst:
+// 1 KiB pieces (16 B/lane) while contiguous, per-lane modular dwords if it wraps.
+// Called by one wave; lands by the wave's next vmcnt(0) (the next barrier).
+__device__ __forceinline__ void dma_row_f32(unsigned char *dst, const float *row, int start, int cover_bytes, int n,
+                                            bool small_n, int lane)
+{
+    if (!small_n && start + cover_bytes / 4 <= n) {
+        const char *src = reinterpret_cast<const char *>(row + start);
+        int off = 0;
+        for (; off + 1024 <= cover_bytes; off += 1024)
+            __builtin_amdgcn_global_load_lds((const void *)(src + off + 16 * lane),
+                                             (__attribute__((address_space(3))) void *)(dst + off), 16, 0, 0);
+        for (; off < cover_bytes; off += 256)
+            __builtin_amdgcn_global_load_lds((const void *)(src + off + 4 * lane),
+                                             (__attribute__((address_space(3))) void *)(dst + off), 4, 0, 0);
+    } else {
+        for (int off = 0; off < cover_bytes; off += 256) {
+            int idx = start + (off >> 2) + lane;
+            if (small_n) {
+                idx %= n;
+            } else {
+                idx = idx >= n ? idx - n : idx;
+            }
+            __builtin_amdgcn_global_load_lds((const void *)(row + idx),
+                                             (__attribute__((address_space(3))) void *)(dst + off), 4, 0, 0);
+        }
+    }
+}
+
+// Slot record stride (int32): len, dst, gs, c0, G sources, padded to a whole s_load.
+__host__ __device__ constexpr int slot_meta_stride(int G) { return G <= 4 ? 8 : 16; }
+
+template <typename Tin, int G, bool PLANE, bool STATS>
+__global__ void __launch_bounds__(kSThreads, 4)
+dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__restrict__ tile_stages,
+                  const i32x4 *__restrict__ stages, const int32_t *__restrict__ slots,
+                  const int32_t *__restrict__ base_tab, const u32x8 *__restrict__ rec_tab)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr bool kDma = std::is_same<Tin, float>::value;
     constexpr int K = 8;
     constexpr int TT = 64 * K;
     constexpr int D = kD;
-    const int ndt = a.o.ndt;
+    constexpr int MS = slot_meta_stride(G);
+    constexpr int U = 4;  // build: elements per lane per pass (independent reads in flight)
+    typedef int32_t meta_t __attribute__((ext_vector_type(MS)));
+    const DedispArgs &o = a.o;
+    const int ndt = o.ndt;
     const int wg = pu::xcd_remap(blockIdx.x, gridDim.x);
     const int dt = wg % ndt;
-    const int tt = a.tt0 + wg / ndt;
+    const int tt = wg / ndt;
     const int t0 = tt * TT;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int first = ld_uniform(tile_first + dt);
-    const int cnt = ld_uniform(tile_count + dt);
-    const int rowlen = ld_uniform(tile_rowlen + dt);
-    const i32x2 tc = ld_uniform(tile_chunks + dt);   // {first chunk, chunk count}
+    const i32x4 tile = ld_uniform(tiles + dt);        // {first trial, count, raw row length, copy bytes}
+    const i32x2 ts = ld_uniform(tile_stages + dt);    // {first stage, stage count}
+    const int first = tile.x, cnt = tile.y;
+    const int copy_bytes = tile.w;
     const int slot0 = wave * D;
     const bool active = slot0 < cnt;
+    const int n = o.n;
+    const bool small_n = o.small_n != 0;
+    const Tin *data = reinterpret_cast<const Tin *>(o.data);
     const uint32_t smem_addr = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char *)smem;
-    const int cover_bytes = (rowlen * 4 + 255) & ~255;
-    const int copy_bytes = group_copy_bytes(rowlen);  // per tile: slot = 2 alignment copies
-    const int slot_bytes = 2 * copy_bytes;
-    const float *rows = a.rows + (t0 - a.T0);
+    float *slot_lds = reinterpret_cast<float *>(smem + a.slot_area);
+    const float *raw_lds = reinterpret_cast<const float *>(smem);
 
     float acc[D][K];
 #pragma unroll
@@ -551,59 +572,102 @@ dedisp_group_kernel(GroupArgs a, const int32_t *__restrict__ tile_first, const i
 #pragma unroll
         for (int k = 0; k < K; ++k) acc[d][k] = 0.0f;
 
-    const u32x8 *recs = rec_tab + (size_t)dt * a.ngroups * kWaves + wave;
+    const u32x8 *recs = rec_tab + (size_t)dt * a.ngroups * kSWaves + wave;
 
-    // ---- LDS-DMA of chunk k's slots into ring buffer b: job j = (slot, copy q)
-    auto issue_dma = [&](int k, int b) {
-        const i32x4 ch = ld_uniform(chunks + tc.x + k);  // {group begin, group end, slot begin, slot end}
-        const int njobs = 2 * (ch.w - ch.z);
-        for (int j = wave; j < njobs; j += kWaves) {
-            const i32x2 sl = ld_uniform(slots + ch.z + (j >> 1));  // {row id, start}
-            const int q = j & 1;
-            const char *src = reinterpret_cast<const char *>(rows + (size_t)sl.x * a.ldr + sl.y + q);
-            unsigned char *dst = smem + b * a.buf_bytes + (j >> 1) * slot_bytes + q * copy_bytes;
-            int off = 0;
-            for (; off + 1024 <= cover_bytes; off += 1024)
-                __builtin_amdgcn_global_load_lds((const void *)(src + off + 16 * lane),
-                                                 (__attribute__((address_space(3))) void *)(dst + off), 16, 0, 0);
-            for (; off < cover_bytes; off += 256)
-                __builtin_amdgcn_global_load_lds((const void *)(src + off + 4 * lane),
-                                                 (__attribute__((address_space(3))) void *)(dst + off), 4, 0, 0);
+    // ---- DMA mode: the channel rows of stage k into the raw area (one buffer)
+    auto issue_raw = [&](int k) {
+        const i32x4 st = ld_uniform(stages + ts.x + k);  // {group begin, group end, slot begin, slot end}
+        const int c0 = st.x * G;
+        const int nc = min(st.y * G, o.nchan) - c0;
+        const int cover_bytes = (tile.z * 4 + 255) & ~255;
+        const int32_t *base = base_tab + (size_t)dt * o.nchan;
+        for (int ci = wave; ci < nc; ci += kSWaves) {
+            const int c = c0 + ci;
+            int start = ld_uniform(base + c) + t0;
+            if (start >= n) start -= n;
+            dma_row_f32(smem + (size_t)ci * a.raw_stride * 4,
+                        reinterpret_cast<const float *>(data) + (size_t)c * (size_t)o.ld, start, cover_bytes, n,
+                        small_n, lane);
         }
     };
 
-    issue_dma(0, 0);
-    for (int k = 0; k < tc.y; ++k) {
-        const int b = k & 1;
-        __syncthreads();  // this wave's DMA landed (vmcnt) and every wave left the other buffer
-        if (k + 1 < tc.y) issue_dma(k + 1, b ^ 1);
+    // ---- build the stage's slots, one slot per wave at a time: R[i] (i < len) at
+    // copy 0 [i] and copy 1 [i - 1]; U elements per lane per pass, all reads first
+    auto build = [&](const i32x4 st) {
+        auto load = [&](const meta_t &m, int q, int i) -> float {
+            if constexpr (kDma) {
+                return raw_lds[m[4 + q] + i];
+            } else {
+                int pos = m[4 + q] + t0 + i;
+                if (small_n) {
+                    pos %= n;
+                } else {
+                    if (pos >= n) pos -= n;
+                    if (pos >= n) pos -= n;
+                }
+                return static_cast<float>(data[(size_t)(m[3] + q) * (size_t)o.ld + pos]);
+            }
+        };
+        for (int s = st.z + wave; s < st.w; s += kSWaves) {
+            const meta_t m = ld_uniform(reinterpret_cast<const meta_t *>(slots + (size_t)s * MS));
+            const int len = m[0], gs = m[2];
+            float *out0 = slot_lds + m[1] / 4;
+            float *out1 = out0 + copy_bytes / 4 - 1;  // out1[0] lands in copy 0's padding
+            for (int i0 = 0; i0 < len; i0 += 64 * U) {
+                int idx[U];
+                float r[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    idx[u] = min(i0 + 64 * u + lane, len - 1);  // clamped: reads stay branch-free
+                    r[u] = 0.0f;
+                }
+                if (gs == G) {
+                    float v[G][U];
+#pragma unroll
+                    for (int q = 0; q < G; ++q)
+#pragma unroll
+                        for (int u = 0; u < U; ++u) v[q][u] = load(m, q, idx[u]);
+#pragma unroll
+                    for (int q = 0; q < G; ++q)
+#pragma unroll
+                        for (int u = 0; u < U; ++u) r[u] += v[q][u];
+                } else {
+                    for (int q = 0; q < gs; ++q)
+#pragma unroll
+                        for (int u = 0; u < U; ++u) r[u] += load(m, q, idx[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int i = i0 + 64 * u + lane;
+                    if (i < len) {
+                        out0[i] = r[u];
+                        out1[i] = r[u];
+                    }
+                }
+            }
+        }
+    };
+
+    if constexpr (kDma) issue_raw(0);
+    for (int k = 0; k < ts.y; ++k) {
+        const i32x4 st = ld_uniform(stages + ts.x + k);
+        __syncthreads();  // raw rows of stage k landed (vmcnt); every wave left the slot area
+        build(st);
+        __syncthreads();  // slots built; every wave left the raw rows
+        if constexpr (kDma) {
+            if (k + 1 < ts.y) issue_raw(k + 1);  // lands while this stage is summed
+        }
         if (!active) continue;
-        const i32x4 ch = ld_uniform(chunks + tc.x + k);
-        const int g0 = ch.x, ng = ch.y - ch.x;
-        const uint32_t base = smem_addr + (uint32_t)(b * a.buf_bytes) + 8u * lane;
-        double w0[4], w1[4];
-        const u32x8 *rc = recs + (size_t)g0 * kWaves;
-        u32x8 rec0 = ld_uniform(rc);
-        u32x8 rec1 = ng > 1 ? ld_uniform(rc + kWaves) : rec0;
-        read_window(w0, base + (rec0[0] & 0x7fffffffu));
-        for (int gi = 0; gi < ng; gi += 2) {
-            const bool has1 = gi + 1 < ng, has2 = gi + 2 < ng, has3 = gi + 3 < ng;
-            u32x8 rec2 = rec0, rec3 = rec1;
-            if (has2) rec2 = ld_uniform(rc + (size_t)(gi + 2) * kWaves);
-            if (has1) prefetch_window(w1, base + (rec1[0] & 0x7fffffffu));
-            group_trials(acc, w0, rec0, base);
-            if (!has1) break;
-            wait_window(w1);
-            if (has3) rec3 = ld_uniform(rc + (size_t)(gi + 3) * kWaves);
-            if (has2) prefetch_window(w0, base + (rec2[0] & 0x7fffffffu));
-            group_trials(acc, w1, rec1, base);
-            if (has2) wait_window(w0);
-            rec0 = rec2;
-            rec1 = rec3;
+        const uint32_t sb = smem_addr + (uint32_t)a.slot_area + 8u * lane;
+        u32x8 rec = ld_uniform(recs + (size_t)st.x * kSWaves);
+        for (int g = st.x; g < st.y; ++g) {
+            const u32x8 next = g + 1 < st.y ? ld_uniform(recs + (size_t)(g + 1) * kSWaves) : rec;
+            group_trials(acc, rec, sb);
+            rec = next;
         }
     }
     if (!active) return;
-    write_outputs<float, float, K, PLANE, STATS>(acc, a.o, first, slot0, cnt, t0, tt, lane);
+    write_outputs<float, float, K, PLANE, STATS>(acc, o, first, slot0, cnt, t0, tt, lane);
 }
 
 // One workgroup per trial: combine the per-time-tile partials in a fixed order
@@ -714,17 +778,18 @@ struct pu_plan {
     size_t lds_bytes = 0;
     int32_t *d_first = nullptr, *d_count = nullptr, *d_rowlen = nullptr, *d_base = nullptr;
     u32x4 *d_rec = nullptr;
-    // group mode (group > 1): rows of exact partial sums, built per time segment
-    int group = 1, ngroups = 0, nrows = 0, nseg = 1, seg_len = 0, row_len = 0, buf_bytes = 0, max_span = 0;
-    int64_t nchunks = 0, nslots = 0;
-    float *d_rows = nullptr;
-    int32_t *d_rowmeta = nullptr;
-    i32x2 *d_tile_chunks = nullptr, *d_slots = nullptr;
-    i32x4 *d_chunks = nullptr;
+    // subband mode (group > 1): per tile {first, count, raw row length, copy bytes},
+    // stages {group begin, group end, slot begin, slot end}, slot records, window records
+    int group = 1, ngroups = 0, nslots_total = 0, raw_stride = 0;
+    size_t slot_area = 0;
+    int64_t nstages = 0;
+    i32x4 *d_tiles = nullptr, *d_stages = nullptr;
+    i32x2 *d_tile_stages = nullptr;
+    int32_t *d_slots = nullptr;
     u32x8 *d_rec8 = nullptr;
-    // optional kernel timing: events before the first launch, after the first row
-    // build (single-segment plans) and after the last launch of each dispatch
-    std::vector<hipEvent_t> ev_start, ev_mid, ev_stop;
+    // optional kernel timing: events before the first and after the last launch of
+    // each dispatch
+    std::vector<hipEvent_t> ev_start, ev_stop;
     int64_t launches = 0;
 };
 
@@ -773,65 +838,52 @@ int dispatch_variant(const pu_plan *p, const DedispArgs &a, bool plane, hipStrea
     return PU_EINVAL;
 }
 
-template <typename Tin>
-void launch_rows(const pu_plan *p, const RowsArgs &ra, hipStream_t s)
+template <typename Tin, int G>
+int launch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
 {
-    const int64_t nblk = (int64_t)((ra.len + 1023) / 1024) * ra.nrows;
-    hipLaunchKernelGGL(build_rows_kernel<Tin>, dim3((unsigned)nblk), dim3(256), 0, s, ra);
+    SubArgs sa{};
+    sa.o = a;
+    sa.ngroups = p->ngroups;
+    sa.raw_stride = p->raw_stride;
+    sa.slot_area = (int32_t)p->slot_area;
+    const dim3 grid((unsigned)((int64_t)p->ndt * p->ntt)), block(kSThreads);
+    if (plane) {
+        auto kern = dedisp_sub_kernel<Tin, G, true, false>;
+        int rc = ensure_lds(kern, p->lds_bytes);
+        if (rc) return rc;
+        hipLaunchKernelGGL(kern, grid, block, p->lds_bytes, s, sa, p->d_tiles, p->d_tile_stages, p->d_stages,
+                           p->d_slots, p->d_base, p->d_rec8);
+    } else {
+        auto kern = dedisp_sub_kernel<Tin, G, false, true>;
+        int rc = ensure_lds(kern, p->lds_bytes);
+        if (rc) return rc;
+        hipLaunchKernelGGL(kern, grid, block, p->lds_bytes, s, sa, p->d_tiles, p->d_tile_stages, p->d_stages,
+                           p->d_slots, p->d_base, p->d_rec8);
+    }
+    return pu::launch_check("dedisp_sub_kernel");
 }
 
-// Group mode: per time segment, build the rows then sum them.
-int dispatch_group(pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s, hipEvent_t mid)
+template <typename Tin>
+int launch_sub_g(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
 {
-    RowsArgs ra{};
-    ra.data = a.data;
-    ra.ld = a.ld;
-    ra.meta = p->d_rowmeta;
-    ra.rows = p->d_rows;
-    ra.ldr = p->row_len;
-    ra.n = (int32_t)p->n;
-    ra.G = p->group;
-    ra.nrows = p->nrows;
-    ra.len = p->row_len;
-    ra.small_n = p->row_len > p->n ? 1 : 0;
-    GroupArgs ga{};
-    ga.o = a;
-    ga.rows = p->d_rows;
-    ga.ldr = p->row_len;
-    ga.ngroups = p->ngroups;
-    ga.buf_bytes = p->buf_bytes;
-    const int tps = p->seg_len / p->TT;  // time tiles per segment
-    for (int sg = 0; sg < p->nseg; ++sg) {
-        ra.T0 = sg * p->seg_len;
-        switch (p->dtype) {
-        case PU_U8: launch_rows<uint8_t>(p, ra, s); break;
-        case PU_F32: launch_rows<float>(p, ra, s); break;
-        default: launch_rows<double>(p, ra, s); break;
-        }
-        int rc = pu::launch_check("build_rows_kernel");
-        if (rc) return rc;
-        if (mid && sg == 0 && p->nseg == 1) PU_TRY_HIP(hipEventRecord(mid, s));
-        ga.T0 = ra.T0;
-        ga.tt0 = sg * tps;
-        const int ntt_seg = std::min(p->ntt - ga.tt0, tps);
-        const dim3 grid((unsigned)((int64_t)p->ndt * ntt_seg)), block(kThreads);
-        if (plane) {
-            auto kern = dedisp_group_kernel<true, false>;
-            rc = ensure_lds(kern, p->lds_bytes);
-            if (rc) return rc;
-            hipLaunchKernelGGL(kern, grid, block, p->lds_bytes, s, ga, p->d_first, p->d_count, p->d_rowlen,
-                               p->d_tile_chunks, p->d_chunks, p->d_slots, p->d_rec8);
-        } else {
-            auto kern = dedisp_group_kernel<false, true>;
-            rc = ensure_lds(kern, p->lds_bytes);
-            if (rc) return rc;
-            hipLaunchKernelGGL(kern, grid, block, p->lds_bytes, s, ga, p->d_first, p->d_count, p->d_rowlen,
-                               p->d_tile_chunks, p->d_chunks, p->d_slots, p->d_rec8);
-        }
-        rc = pu::launch_check("dedisp_group_kernel");
-        if (rc) return rc;
+    switch (p->group) {
+    case 2: return launch_sub<Tin, 2>(p, a, plane, s);
+    case 4: return launch_sub<Tin, 4>(p, a, plane, s);
+    case 8: return launch_sub<Tin, 8>(p, a, plane, s);
     }
-    return PU_OK;
+    pu::set_error("bad plan group %d", p->group);
+    return PU_EINVAL;
+}
+
+int dispatch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
+{
+    switch (p->dtype) {
+    case PU_U8: return launch_sub_g<uint8_t>(p, a, plane, s);
+    case PU_F32: return launch_sub_g<float>(p, a, plane, s);
+    case PU_F64: return launch_sub_g<double>(p, a, plane, s);
+    }
+    pu::set_error("bad plan dtype");
+    return PU_EINVAL;
 }
 
 int dispatch(pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
@@ -839,8 +891,7 @@ int dispatch(pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
     const size_t nslot = p->ev_start.size();
     const size_t slot = nslot ? (size_t)(p->launches % (int64_t)nslot) : 0;
     if (nslot) PU_TRY_HIP(hipEventRecord(p->ev_start[slot], s));
-    int rc = p->group > 1 ? dispatch_group(p, a, plane, s, nslot ? p->ev_mid[slot] : nullptr)
-                          : dispatch_variant(p, a, plane, s);
+    int rc = p->group > 1 ? dispatch_sub(p, a, plane, s) : dispatch_variant(p, a, plane, s);
     if (rc) return rc;
     if (nslot) PU_TRY_HIP(hipEventRecord(p->ev_stop[slot], s));
     ++p->launches;
@@ -849,7 +900,7 @@ int dispatch(pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
 
 void destroy_events(pu_plan *p)
 {
-    for (auto *v : {&p->ev_start, &p->ev_mid, &p->ev_stop}) {
+    for (auto *v : {&p->ev_start, &p->ev_stop}) {
         for (auto e : *v) (void)hipEventDestroy(e);
         v->clear();
     }
@@ -864,11 +915,10 @@ void free_plan(pu_plan *p)
     (void)hipFree(p->d_rowlen);
     (void)hipFree(p->d_base);
     (void)hipFree(p->d_rec);
-    (void)hipFree(p->d_rows);
-    (void)hipFree(p->d_rowmeta);
-    (void)hipFree(p->d_tile_chunks);
+    (void)hipFree(p->d_tiles);
+    (void)hipFree(p->d_tile_stages);
+    (void)hipFree(p->d_stages);
     (void)hipFree(p->d_slots);
-    (void)hipFree(p->d_chunks);
     (void)hipFree(p->d_rec8);
     delete p;
 }
@@ -991,223 +1041,234 @@ int plan_channels(pu_plan *p, const int64_t *shifts, size_t budget)
     return rc;
 }
 
-// ---- group mode planning (float32 accumulation variants).  Returns PU_EUNSUPPORTED
-// when the trial grid does not suit grouping (the caller then plans channel mode).
-constexpr int kRowSpan = 2048;   // max first-channel shift range served by one row
+// ---- subband mode planning (float32 accumulation).  Returns PU_EUNSUPPORTED when one
+// trial's group does not fit the LDS budget (the caller then tries a smaller G, then
+// channel mode).
+constexpr int64_t kSubMaxSpread = 2048;
 
-struct SlotAcc {
-    int32_t row, lo, hi;
+struct SubSlot {
+    int32_t vid;     // relative-shift vector id (per group)
+    int64_t lo, hi;  // first-channel shift range of the tile's trials with this vector
+    int64_t d0;      // one trial with this vector
 };
 
-int plan_group(pu_plan *p, const int64_t *shifts, int G, size_t budget, size_t mem_cap)
+int plan_sub(pu_plan *p, const int64_t *shifts, int G, size_t budget)
 {
     const int64_t nchan = p->nchan, n = p->n, ndm = p->ndm;
-    const int TT = p->TT;
+    const int64_t TT = p->TT;
     const int ngroups = (int)((nchan + G - 1) / G);
-    const int buf_bytes = (int)(budget / 2) & ~255;
-    std::vector<int32_t> sn((size_t)(ndm * nchan));
-    for (size_t i = 0; i < sn.size(); ++i) {
-        int64_t v = shifts[i] % n;
-        sn[i] = (int32_t)(v < 0 ? v + n : v);
-    }
-    // ---- rows: distinct relative-shift vectors per group, each split into clusters of
-    // first-channel shifts (circularly) no wider than kRowSpan
-    std::vector<int32_t> rowid((size_t)(ndm * ngroups)), roff((size_t)(ndm * ngroups));
-    std::vector<int32_t> meta;
-    int nrows = 0, max_span = 0;
-    std::vector<int32_t> order((size_t)ndm), bs;
-    for (int g = 0; g < ngroups; ++g) {
-        const int64_t c0 = (int64_t)g * G;
-        const int gs = (int)std::min<int64_t>(G, nchan - c0);
-        auto vec = [&](int64_t d, int k) {
-            int32_t v = sn[d * nchan + c0 + k] - sn[d * nchan + c0];
-            return v < 0 ? v + (int32_t)n : v;
-        };
-        auto base_of = [&](int64_t d) { return sn[d * nchan + c0]; };
-        for (int64_t d = 0; d < ndm; ++d) order[d] = (int32_t)d;
-        std::sort(order.begin(), order.end(), [&](int32_t x, int32_t y) {
-            for (int k = 1; k < gs; ++k) {
-                const int32_t a = vec(x, k), b = vec(y, k);
-                if (a != b) return a < b;
-            }
-            if (base_of(x) != base_of(y)) return base_of(x) < base_of(y);
-            return x < y;
-        });
-        for (int64_t a = 0; a < ndm;) {
-            int64_t b = a + 1;
-            while (b < ndm) {
-                bool same = true;
-                for (int k = 1; k < gs && same; ++k) same = vec(order[a], k) == vec(order[b], k);
-                if (!same) break;
-                ++b;
-            }
-            const int64_t m = b - a;
-            // start after the widest circular gap between consecutive (sorted) bases
-            int64_t start = 0, gap = base_of(order[a]) + n - base_of(order[b - 1]);
-            for (int64_t i = 0; i + 1 < m; ++i) {
-                const int64_t gi = base_of(order[a + i + 1]) - base_of(order[a + i]);
-                if (gi > gap) {
-                    gap = gi;
-                    start = i + 1;
+    const bool dma = p->dtype == PU_F32;
+    const int64_t raw_cap = dma ? (int64_t)budget / 2 : 0;
+    const int64_t slot_cap = (int64_t)budget - raw_cap;
+    auto S = [&](int64_t d, int64_t c) { return shifts[d * nchan + c]; };
+    auto raw_stride_of = [&](int64_t spread) { return (TT + spread + 1 + 63) / 64 * 64; };
+    // slot copy: len = TT + span + 1 elements, + 1 padding float (build writes copy 1's
+    // element -1 there)
+    auto copy_of = [&](int64_t span) { return (TT + span + 2 + 63) / 64 * 64 * 4; };
+    if (dma && G * raw_stride_of(0) * 4 > raw_cap) return PU_EUNSUPPORTED;
+    if (2 * copy_of(0) > slot_cap) return PU_EUNSUPPORTED;
+
+    // ---- relative-shift vector id per (trial, group): v_k = s[c0 + k] - s[c0], k < gs
+    std::vector<int32_t> vid((size_t)(ndm * ngroups));
+    {
+        std::vector<int64_t> order((size_t)ndm);
+        for (int g = 0; g < ngroups; ++g) {
+            const int64_t c0 = (int64_t)g * G;
+            const int gs = (int)std::min<int64_t>(G, nchan - c0);
+            auto cmp = [&](int64_t x, int64_t y) {
+                for (int k = 1; k < gs; ++k) {
+                    const int64_t u = S(x, c0 + k) - S(x, c0), v = S(y, c0 + k) - S(y, c0);
+                    if (u != v) return u < v ? -1 : 1;
                 }
+                return 0;
+            };
+            for (int64_t d = 0; d < ndm; ++d) order[d] = d;
+            std::sort(order.begin(), order.end(), [&](int64_t x, int64_t y) {
+                const int c = cmp(x, y);
+                return c != 0 ? c < 0 : x < y;
+            });
+            int32_t id = -1;
+            for (int64_t i = 0; i < ndm; ++i) {
+                if (i == 0 || cmp(order[i], order[i - 1]) != 0) ++id;
+                vid[(size_t)order[i] * ngroups + g] = id;
             }
-            int32_t lo = 0;
-            bool open = false;
-            for (int64_t i = 0; i < m; ++i) {
-                const int32_t d = order[a + (start + i) % m];
-                const int32_t bd = base_of(d);
-                int64_t rel = open ? (bd - lo + n) % n : 0;
-                if (!open || rel > kRowSpan) {
-                    lo = bd;
-                    rel = 0;
-                    open = true;
-                    meta.push_back((int32_t)c0);
-                    meta.push_back(gs);
-                    meta.push_back(lo);
-                    for (int k = 1; k < G; ++k) meta.push_back(k < gs ? vec(d, k) : 0);
-                    ++nrows;
-                }
-                rowid[(size_t)d * ngroups + g] = nrows - 1;
-                roff[(size_t)d * ngroups + g] = (int32_t)rel;
-                max_span = std::max(max_span, (int)rel);
-            }
-            a = b;
         }
     }
-    // ---- DM tiles: <= kTPT consecutive trials; every group's slots (distinct rows of the
-    // tile) must fit one ring buffer at the tile's row length
-    std::vector<int32_t> first, count, rowlen;
-    std::vector<std::vector<SlotAcc>> tslots;  // per tile * ngroups
+
+    // ---- DM tiles: <= kSTPT consecutive trials whose channel rows (one group's worth)
+    // fit the raw area and whose slots of any one group fit the slot area
+    std::vector<int32_t> first, count;
+    std::vector<int64_t> spread_t, span_t, smin_t;  // smin_t: per tile x channel
+    std::vector<std::vector<SubSlot>> tslots;       // per tile x group
     {
-        std::vector<std::vector<SlotAcc>> cur((size_t)ngroups), nxt((size_t)ngroups);
+        std::vector<int64_t> mn((size_t)nchan), mx((size_t)nchan);
+        std::vector<std::vector<SubSlot>> cur((size_t)ngroups), nxt((size_t)ngroups);
         int64_t i = 0;
         while (i < ndm) {
-            int spread = 0;
+            for (int64_t c = 0; c < nchan; ++c) mn[c] = mx[c] = S(i, c);
             for (int g = 0; g < ngroups; ++g) {
-                const size_t k = (size_t)i * ngroups + g;
-                cur[g].assign(1, SlotAcc{rowid[k], roff[k], roff[k]});
+                const int64_t b = S(i, (int64_t)g * G);
+                cur[g].assign(1, SubSlot{vid[(size_t)i * ngroups + g], b, b, i});
             }
+            int64_t spread = 0, span = 0;
             int64_t j = i + 1;
-            while (j < ndm && j - i < kTPT) {
-                int sp = spread;
+            while (j < ndm && j - i < kSTPT) {
+                int64_t sp = spread;
+                for (int64_t c = 0; c < nchan; ++c)
+                    sp = std::max(sp, std::max(mx[c], S(j, c)) - std::min(mn[c], S(j, c)));
+                if (sp > kSubMaxSpread) break;
+                if (dma && G * raw_stride_of(sp) * 4 > raw_cap) break;
+                int64_t spn = span;
                 size_t maxslots = 0;
                 for (int g = 0; g < ngroups; ++g) {
-                    const size_t k = (size_t)j * ngroups + g;
                     nxt[g] = cur[g];
+                    const int32_t v = vid[(size_t)j * ngroups + g];
+                    const int64_t b = S(j, (int64_t)g * G);
                     bool found = false;
-                    for (auto &sa : nxt[g])
-                        if (sa.row == rowid[k]) {
-                            sa.lo = std::min(sa.lo, roff[k]);
-                            sa.hi = std::max(sa.hi, roff[k]);
-                            sp = std::max(sp, sa.hi - sa.lo);
+                    for (auto &sl : nxt[g])
+                        if (sl.vid == v) {
+                            sl.lo = std::min(sl.lo, b);
+                            sl.hi = std::max(sl.hi, b);
+                            spn = std::max(spn, sl.hi - sl.lo);
                             found = true;
+                            break;
                         }
-                    if (!found) nxt[g].push_back(SlotAcc{rowid[k], roff[k], roff[k]});
+                    if (!found) nxt[g].push_back(SubSlot{v, b, b, j});
                     maxslots = std::max(maxslots, nxt[g].size());
                 }
-                if (sp > kMaxSpread || maxslots * 2 * (size_t)group_copy_bytes(TT + sp) > (size_t)buf_bytes) break;
+                if ((int64_t)maxslots * 2 * copy_of(spn) > slot_cap) break;
+                for (int64_t c = 0; c < nchan; ++c) {
+                    mn[c] = std::min(mn[c], S(j, c));
+                    mx[c] = std::max(mx[c], S(j, c));
+                }
                 std::swap(cur, nxt);
                 spread = sp;
+                span = spn;
                 ++j;
-            }
-            size_t maxslots = 0;
-            for (int g = 0; g < ngroups; ++g) maxslots = std::max(maxslots, cur[g].size());
-            if (maxslots * 2 * (size_t)group_copy_bytes(TT + spread) > (size_t)buf_bytes) {
-                pu::set_error("group mode: slots of one trial exceed the LDS buffer");
-                return PU_EUNSUPPORTED;
             }
             first.push_back((int32_t)i);
             count.push_back((int32_t)(j - i));
-            rowlen.push_back(TT + spread);
+            spread_t.push_back(spread);
+            span_t.push_back(span);
+            smin_t.insert(smin_t.end(), mn.begin(), mn.end());
             for (int g = 0; g < ngroups; ++g) tslots.push_back(cur[g]);
-            p->max_spread = std::max(p->max_spread, spread);
             i = j;
         }
     }
     const int ndt = (int)first.size();
-    // ---- chunks (groups whose slots fit one buffer), slots, window records
-    std::vector<i32x2> tile_chunks((size_t)ndt), slots;
-    std::vector<i32x4> chunks;
-    std::vector<u32x8> rec((size_t)ndt * ngroups * kWaves);
-    std::vector<int32_t> slot_in_chunk((size_t)ngroups);
+    int64_t raw_stride = 64, max_spread = 0;
     for (int t = 0; t < ndt; ++t) {
-        const uint32_t copy_bytes = (uint32_t)group_copy_bytes(rowlen[t]);
-        const int cap = (int)((uint32_t)buf_bytes / (2 * copy_bytes));
-        tile_chunks[t] = i32x2{(int32_t)chunks.size(), 0};
+        raw_stride = std::max(raw_stride, raw_stride_of(spread_t[t]));
+        max_spread = std::max(max_spread, spread_t[t]);
+    }
+    // channels one stage may stage (>= G: the widest tile passed G * its stride <= raw_cap)
+    const int64_t chan_cap = dma ? raw_cap / (raw_stride * 4) : (int64_t)INT32_MAX;
+
+    // ---- stages (consecutive groups whose channels and slots fit), slot records, window
+    // records, DMA row bases
+    const int ms = slot_meta_stride(G);
+    std::vector<i32x4> tiles((size_t)ndt), stages;
+    std::vector<i32x2> tile_stages((size_t)ndt);
+    std::vector<int32_t> slotmeta, base;
+    std::vector<u32x8> rec((size_t)ndt * ngroups * kSWaves);
+    std::vector<int64_t> slot_local((size_t)ngroups);
+    int64_t slot_used = 0, max_stage_chans = 0;
+    for (int t = 0; t < ndt; ++t) {
+        const int64_t cb = copy_of(span_t[t]);
+        const int64_t *smin = smin_t.data() + (size_t)t * nchan;
+        tiles[t] = i32x4{first[t], count[t], (int32_t)(TT + spread_t[t] + 1), (int32_t)cb};
+        if (dma)
+            for (int64_t c = 0; c < nchan; ++c) {
+                int64_t b = smin[c] % n;
+                base.push_back((int32_t)(b < 0 ? b + n : b));
+            }
+        tile_stages[t] = i32x2{(int32_t)stages.size(), 0};
         int g = 0;
         while (g < ngroups) {
-            const int s_begin = (int)slots.size();
-            int used = 0, g_end = g;
-            while (g_end < ngroups && used + (int)tslots[(size_t)t * ngroups + g_end].size() <= cap) {
-                slot_in_chunk[g_end] = used;
-                for (const auto &sa : tslots[(size_t)t * ngroups + g_end]) slots.push_back(i32x2{sa.row, sa.lo});
-                used += (int)tslots[(size_t)t * ngroups + g_end].size();
+            const int32_t s_begin = (int32_t)(slotmeta.size() / ms);
+            int64_t used = 0, chans = 0;
+            int g_end = g;
+            while (g_end < ngroups) {
+                const int64_t c0 = (int64_t)g_end * G;
+                const int gs = (int)std::min<int64_t>(G, nchan - c0);
+                const auto &sls = tslots[(size_t)t * ngroups + g_end];
+                const int64_t ns = (int64_t)sls.size();
+                if (g_end > g && (chans + gs > chan_cap || (used + ns) * 2 * cb > slot_cap)) break;
+                slot_local[g_end] = used;
+                for (const auto &sl : sls) {
+                    slotmeta.push_back((int32_t)(TT + (sl.hi - sl.lo) + 1));
+                    slotmeta.push_back((int32_t)(used * 2 * cb));
+                    slotmeta.push_back(gs);
+                    slotmeta.push_back((int32_t)c0);
+                    for (int k = 0; k < ms - 4; ++k) {
+                        int64_t src = 0;
+                        if (k < gs) {
+                            // smallest shift of channel c0+k over the slot's trials
+                            const int64_t sk = sl.lo + S(sl.d0, c0 + k) - S(sl.d0, c0);
+                            if (dma) {
+                                src = (chans + k) * raw_stride + (sk - smin[c0 + k]);
+                            } else {
+                                src = sk % n;
+                                if (src < 0) src += n;
+                            }
+                        }
+                        slotmeta.push_back((int32_t)src);
+                    }
+                    ++used;
+                }
+                chans += gs;
                 ++g_end;
             }
-            chunks.push_back(i32x4{g, g_end, s_begin, (int32_t)slots.size()});
-            tile_chunks[t][1]++;
+            stages.push_back(i32x4{g, g_end, s_begin, (int32_t)(slotmeta.size() / ms)});
+            tile_stages[t][1]++;
+            slot_used = std::max(slot_used, used * 2 * cb);
+            max_stage_chans = std::max(max_stage_chans, chans);
             g = g_end;
         }
-        for (g = 0; g < ngroups; ++g) {
-            const auto &sl = tslots[(size_t)t * ngroups + g];
-            for (int w = 0; w < kWaves; ++w) {
+        for (int gg = 0; gg < ngroups; ++gg) {
+            const auto &sls = tslots[(size_t)t * ngroups + gg];
+            for (int w = 0; w < kSWaves; ++w) {
                 u32x8 r;
-                uint32_t prev = 0xffffffffu;
                 for (int d = 0; d < kD; ++d) {
-                    const int dd = std::min(w * kD + d, count[t] - 1);  // padding repeats the last trial
-                    const size_t k = (size_t)(first[t] + dd) * ngroups + g;
-                    int si = 0;
-                    while (sl[si].row != rowid[k]) ++si;
-                    const uint32_t s = (uint32_t)(roff[k] - sl[si].lo);
-                    const uint32_t off = (uint32_t)(slot_in_chunk[g] + si) * 2u * copy_bytes + (s & 1u) * copy_bytes +
-                                         (s & ~1u) * 4u;
-                    r[d] = off | (off != prev ? 0x80000000u : 0u);
-                    prev = off;
+                    const int64_t tr = first[t] + std::min(w * kD + d, count[t] - 1);  // padding repeats the last trial
+                    const int32_t v = vid[(size_t)tr * ngroups + gg];
+                    size_t si = 0;
+                    while (sls[si].vid != v) ++si;
+                    const int64_t rr = S(tr, (int64_t)gg * G) - sls[si].lo;
+                    r[d] = (uint32_t)((slot_local[gg] + (int64_t)si) * 2 * cb + (rr & 1) * cb + (rr & ~int64_t(1)) * 4);
                 }
-                rec[((size_t)t * ngroups + g) * kWaves + w] = r;
+                rec[((size_t)t * ngroups + gg) * kSWaves + w] = r;
             }
         }
     }
-    // ---- time segments: the row buffer holds seg_len samples (+ halo) of every row
-    const int64_t ntt = (n + TT - 1) / TT;
-    const int64_t halo = (int64_t)max_span + p->max_spread + 128;
-    int64_t seg_tiles = ntt;
-    while (seg_tiles > 16 && (int64_t)nrows * (seg_tiles * TT + halo) * 4 > (int64_t)mem_cap)
-        seg_tiles = (seg_tiles + 1) / 2;
-    if ((int64_t)nrows * (seg_tiles * TT + halo) * 4 > (int64_t)mem_cap) {
-        pu::set_error("group mode: %d rows exceed the row-buffer cap", nrows);
+    const int64_t raw_used = dma ? (max_stage_chans * raw_stride * 4 + 255) / 256 * 256 : 0;
+    if (raw_used + slot_used > 160 * 1024) {
+        pu::set_error("subband mode: %lld bytes of LDS", (long long)(raw_used + slot_used));
         return PU_EUNSUPPORTED;
     }
-    p->group = G;
-    p->ngroups = ngroups;
-    p->nrows = nrows;
-    p->max_span = max_span;
-    p->seg_len = (int)(seg_tiles * TT);
-    p->nseg = (int)((ntt + seg_tiles - 1) / seg_tiles);
-    p->row_len = (int)((p->seg_len + halo + 63) / 64 * 64);
-    p->buf_bytes = buf_bytes;
-    p->lds_bytes = 2 * (size_t)buf_bytes;
-    p->ndt = ndt;
-    p->ncc = 0;
-    p->row_stride = group_copy_bytes(*std::max_element(rowlen.begin(), rowlen.end())) / 4;
-    p->nchunks = (int64_t)chunks.size();
-    p->nslots = (int64_t)slots.size();
-    if ((int64_t)p->ndt * p->ntt >= (int64_t(1) << 31) || (int64_t)nrows * ((p->row_len + 1023) / 1024) >= (int64_t(1) << 31)) {
+    if ((int64_t)ndt * p->ntt >= (int64_t(1) << 31) || (int64_t)slotmeta.size() >= (int64_t(1) << 31)) {
         pu::set_error("pu_plan_create: grid too large");
         return PU_EINVAL;
     }
+    p->group = G;
+    p->ngroups = ngroups;
+    p->ndt = ndt;
+    p->ncc = (int)max_stage_chans;
+    p->raw_stride = (int)raw_stride;
+    p->row_stride = (int)raw_stride;
+    p->max_spread = (int)max_spread;
+    p->small_n = raw_stride + 2 > n ? 1 : 0;
+    p->slot_area = (size_t)raw_used;
+    p->lds_bytes = (size_t)(raw_used + slot_used);
+    p->nslots_total = (int)(slotmeta.size() / ms);
+    p->nstages = (int64_t)stages.size();
     int rc = PU_OK;
-    if (!rc) rc = upload(&p->d_first, first);
-    if (!rc) rc = upload(&p->d_count, count);
-    if (!rc) rc = upload(&p->d_rowlen, rowlen);
-    if (!rc) rc = upload(&p->d_tile_chunks, tile_chunks);
-    if (!rc) rc = upload(&p->d_chunks, chunks);
-    if (!rc) rc = upload(&p->d_slots, slots);
+    if (!rc) rc = upload(&p->d_tiles, tiles);
+    if (!rc) rc = upload(&p->d_tile_stages, tile_stages);
+    if (!rc) rc = upload(&p->d_stages, stages);
+    if (!rc) rc = upload(&p->d_slots, slotmeta);
     if (!rc) rc = upload(&p->d_rec8, rec);
-    if (!rc) rc = upload(&p->d_rowmeta, meta);
-    if (!rc)
-        rc = pu::hip_check(hipMalloc((void **)&p->d_rows, (size_t)nrows * p->row_len * sizeof(float)),
-                           "hipMalloc(group rows)");
+    if (!rc && dma) rc = upload(&p->d_base, base);
     return rc;
 }
 
@@ -1228,11 +1289,10 @@ void reset_tables(pu_plan *p)
     (void)hipFree(p->d_rowlen);
     (void)hipFree(p->d_base);
     (void)hipFree(p->d_rec);
-    (void)hipFree(p->d_rows);
-    (void)hipFree(p->d_rowmeta);
-    (void)hipFree(p->d_tile_chunks);
+    (void)hipFree(p->d_tiles);
+    (void)hipFree(p->d_tile_stages);
+    (void)hipFree(p->d_stages);
     (void)hipFree(p->d_slots);
-    (void)hipFree(p->d_chunks);
     (void)hipFree(p->d_rec8);
     *p = keep;
 }
@@ -1254,8 +1314,8 @@ int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int
                (long long)n);
     PU_REQUIRE(ndm > 0 && ndm < (1 << 30), "pu_plan_create: ndm %lld out of range", (long long)ndm);
     PU_REQUIRE(shifts != nullptr, "pu_plan_create: shifts is NULL");
-    PU_REQUIRE(group == 0 || group == 1 || group == 2 || group == 4 || group == 8 || group == 16,
-               "pu_plan_create: group %d not in {0 (auto), 1, 2, 4, 8, 16}", group);
+    PU_REQUIRE(group == 0 || group == 1 || group == 2 || group == 4 || group == 8,
+               "pu_plan_create: group %d not in {0 (auto), 1, 2, 4, 8}", group);
     if (dtype == PU_U8 && acc != PU_ACC_F64)
         PU_REQUIRE(nchan <= 65793, "pu_plan_create: u8 f32 accumulation exact only for nchan <= 65793");
 
@@ -1271,11 +1331,9 @@ int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int
     p->TT = 64 * p->K;
     p->ntt = (int)((n + p->TT - 1) / p->TT);
 
-    // LDS budget per workgroup; PU_LDS_BUDGET_KB overrides (tuning)
-    size_t budget = kLdsBudget;
-    if (const char *env = getenv("PU_LDS_BUDGET_KB")) budget = (size_t)std::max(8, atoi(env)) * 1024;
-    size_t mem_cap = size_t(16) << 30;
-    if (const char *env = getenv("PU_ROWS_MB")) mem_cap = (size_t)std::max(1, atoi(env)) << 20;
+    // LDS budget per workgroup (channel / subband mode); PU_LDS_BUDGET_KB overrides (tuning)
+    size_t budget = kLdsBudget, sub_budget = kSubLdsBudget;
+    if (const char *env = getenv("PU_LDS_BUDGET_KB")) budget = sub_budget = (size_t)std::max(8, atoi(env)) * 1024;
     // group size: explicit, else PU_GROUP, else 4; float32 accumulation only (the
     // float64 modes keep the reference's sequential channel order)
     int G = group;
@@ -1283,11 +1341,12 @@ int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int
         G = 4;
         if (const char *env = getenv("PU_GROUP")) G = atoi(env);
     }
+    G = std::min(G, 8);
     if (kVariants[v].acc_f64) G = 1;
     while (G > 1 && G >= nchan) G >>= 1;
     int rc = PU_EUNSUPPORTED;
     for (; G > 1 && rc == PU_EUNSUPPORTED; G >>= 1) {
-        rc = plan_group(p, shifts, G, budget, mem_cap);
+        rc = plan_sub(p, shifts, G, sub_budget);
         if (rc == PU_EUNSUPPORTED) reset_tables(p);
     }
     if (rc == PU_EUNSUPPORTED) rc = plan_channels(p, shifts, budget);
@@ -1310,7 +1369,7 @@ int pu_plan_enable_timing(pu_plan *p, int nslots)
 {
     PU_REQUIRE(p != nullptr && nslots >= 0 && nslots <= 65536, "pu_plan_enable_timing: bad arguments");
     destroy_events(p);
-    for (auto *v : {&p->ev_start, &p->ev_mid, &p->ev_stop}) {
+    for (auto *v : {&p->ev_start, &p->ev_stop}) {
         v->assign((size_t)nslots, nullptr);
         for (int i = 0; i < nslots; ++i) PU_TRY_HIP(hipEventCreate(&(*v)[i]));
     }
@@ -1330,20 +1389,6 @@ int pu_plan_kernel_times(pu_plan *p, float *ms, int n)
     return m;
 }
 
-int pu_plan_phase_times(pu_plan *p, float *build_ms, float *sum_ms, int n)
-{
-    PU_REQUIRE(p != nullptr && build_ms != nullptr && sum_ms != nullptr, "pu_plan_phase_times: bad arguments");
-    if (p->group <= 1 || p->nseg != 1) return 0;
-    const int64_t have = std::min<int64_t>(p->launches, (int64_t)p->ev_start.size());
-    const int m = (int)std::min<int64_t>(n, have);
-    for (int i = 0; i < m; ++i) {
-        PU_TRY_HIP(hipEventSynchronize(p->ev_stop[i]));
-        PU_TRY_HIP(hipEventElapsedTime(&build_ms[i], p->ev_start[i], p->ev_mid[i]));
-        PU_TRY_HIP(hipEventElapsedTime(&sum_ms[i], p->ev_mid[i], p->ev_stop[i]));
-    }
-    return m;
-}
-
 size_t pu_plan_workspace_bytes(const pu_plan *p)
 {
     if (!p) return 0;
@@ -1353,9 +1398,9 @@ size_t pu_plan_workspace_bytes(const pu_plan *p)
 int pu_plan_info(const pu_plan *p, int64_t *info, int n)
 {
     if (!p || !info) return 0;
-    const int64_t v[] = {p->ndm, p->ndt, p->ntt, kTPT, p->TT, p->ncc,
+    const int64_t v[] = {p->ndm, p->ndt, p->ntt, p->group > 1 ? kSTPT : kTPT, p->TT, p->ncc,
                          p->row_stride, (int64_t)p->lds_bytes, kVariants[p->variant].acc_f64, p->max_spread,
-                         p->group, p->nrows, p->nseg, (int64_t)p->nrows * p->row_len * 4, p->nslots};
+                         p->group, p->nslots_total, p->nstages, (int64_t)p->slot_area, p->raw_stride};
     const int m = std::min<int>(n, (int)(sizeof v / sizeof v[0]));
     for (int k = 0; k < m; ++k) info[k] = v[k];
     return m;

@@ -36,7 +36,6 @@ SIGNATURES = {
     "pu_plan_info": (_i32, [_vp, _vp, _i32]),
     "pu_plan_enable_timing": (_i32, [_vp, _i32]),
     "pu_plan_kernel_times": (_i32, [_vp, _vp, _i32]),
-    "pu_plan_phase_times": (_i32, [_vp, _vp, _vp, _i32]),
     "pu_row_sums": (_i32, [_vp, _i32, _i64, _i64, _i64, _i32, _vp, _vp, _f64, _vp, _vp, _sz, _vp]),
     "pu_row_sums_workspace_bytes": (_sz, [_i64, _i64]),
     "pu_col_means": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp]),
@@ -52,8 +51,8 @@ SIGNATURES = {
 }
 
 INFO_FIELDS = ("ndm", "dm_tiles", "time_tiles", "trials_per_tile", "time_tile", "chans_per_step",
-               "row_stride", "lds_bytes", "acc_is_f64", "max_spread", "group", "group_rows", "segments",
-               "row_buffer_bytes", "slots")
+               "row_stride", "lds_bytes", "acc_is_f64", "max_spread", "group", "slots", "stages",
+               "slot_area", "raw_stride")
 
 
 class HipBackendError(RuntimeError):
@@ -152,7 +151,7 @@ class Plan:
 
     def __init__(self, dtype_code_, acc, nchan, nsamples, shifts, group=0):
         """``group``: channels summed per group row (0 = library default, 1 = channel
-        mode, 2/4/8/16); float64 accumulation always uses channel mode."""
+        mode, 2/4/8); float64 accumulation always uses channel mode."""
         require_gpu()
         sh = np.ascontiguousarray(shifts, dtype=np.int64)
         ndm = sh.shape[0]
@@ -208,16 +207,6 @@ class Plan:
         if m < 0:
             check(m, "pu_plan_kernel_times")
         return out[:m]
-
-    def phase_times_ms(self, n):
-        """(row-build ms, group-sum ms) per timed launch (single-segment group plans)."""
-        b = np.zeros(int(n), np.float32)
-        g = np.zeros(int(n), np.float32)
-        m = lib().pu_plan_phase_times(self._h, b.ctypes.data_as(ctypes.c_void_p), g.ctypes.data_as(ctypes.c_void_p),
-                                      int(n))
-        if m < 0:
-            check(m, "pu_plan_phase_times")
-        return b[:m], g[:m]
 
     def dedisperse(self, data, plane=None, stream=None):
         """Dedispersed plane (ndm, nsamples) in the accumulation dtype."""

@@ -41,14 +41,12 @@ for r in range(rounds):
             out = p.search(x, workspace=ws)
         torch.cuda.synchronize()
         ms = p.kernel_times_ms(3)
-        bms, sms = p.phase_times_ms(3)
         res[v].append(float(np.median(ms)))
         snr = out[2].cpu().numpy()
         if ref is None:
             ref = snr
         ok = np.allclose(snr, ref, rtol=1e-5)
-        phase = f" build {np.median(bms):.3f} sum {np.median(sms):.3f}" if len(bms) else ""
-        print(f"round {r} group {v[0]} lds {v[1]}KB: {np.median(ms):.3f} ms{phase} same={ok}", flush=True)
+        print(f"round {r} group {v[0]} lds {v[1]}KB: {np.median(ms):.3f} ms same={ok}", flush=True)
 samples = cfg.nsamples * dms.size
 for v in plans:
     m = float(np.median(res[v]))

@@ -155,20 +155,20 @@ def test_plane_arbitrary_dm_list_large_spread(gpu):
             np.testing.assert_array_equal(pu[k].astype(np.float64), oracle.dedisperse(u, sh[k]))
 
 
-@pytest.mark.parametrize("dt", ["u8", "f32"])
-def test_plane_group_mode_segmented(gpu, dt, monkeypatch):
-    """A row-buffer cap that forces several time segments (build + sum per segment)."""
+@pytest.mark.parametrize("dt", ["u8", "f32", "f64"])
+def test_plane_subband_small_lds_budget(gpu, dt, monkeypatch):
+    """A small LDS budget: one group per stage, short DM tiles, many stages per tile."""
     c = CONFIGS["C5"]
     rng = np.random.default_rng(21)
-    n = 1 << 16
+    n = 1 << 14
     x = rng.random((c.nchan, n)) * 50
-    x = x.astype(np.uint8) if dt == "u8" else x.astype(np.float32)
+    x = {"u8": x.astype(np.uint8), "f32": x.astype(np.float32), "f64": x}[dt]
     dms = np.linspace(c.dmmin, c.dmmax, 90)
     sh = _hip.shift_table(c.nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
-    monkeypatch.setenv("PU_ROWS_MB", "24")
+    monkeypatch.setenv("PU_LDS_BUDGET_KB", "24")
     info = {}
-    plane = _plane(x, sh, "native", 4, info)
-    assert info["group"] == 4 and info["segments"] > 1, info
+    plane = _plane(x, sh, "f32" if dt == "f64" else "native", 4, info)
+    assert info["group"] == 4 and info["stages"] > 2 * info["dm_tiles"], info
     for k in range(0, 90, 7):
         ref = oracle.dedisperse(x, sh[k])
         if dt == "u8":
