@@ -167,13 +167,12 @@ __device__ __forceinline__ void channel_trials(Ta (&acc)[kD][K], double (&w)[4],
 // Outputs of one wave: the dedispersed plane rows of its D trials, or their per-tile
 // partial statistics (1/2/4/8-sample rebinned sums: max, shifted sum, shifted sum of
 // squares; lane-local in the accumulation type, then float64 wave reductions).
-template <typename Tl, typename Ta, int K, bool PLANE, bool STATS>
-__device__ __forceinline__ void write_outputs(const Ta (&acc)[kD][K], const DedispArgs &a, int first, int slot0,
+template <typename Tl, typename Ta, int K, int D, bool PLANE, bool STATS>
+__device__ __forceinline__ void write_outputs(const Ta (&acc)[D][K], const DedispArgs &a, int first, int slot0,
                                               int cnt, int t0, int tt, int lane)
 {
     constexpr int E = 8 / (int)sizeof(Tl);
     constexpr int J = K / E;
-    constexpr int D = kD;
     const int n = a.n;
     // sample index of acc[.][k] for this lane
     auto sample = [&](int k) { return t0 + E * lane + 64 * E * (k / E) + (k % E); };
@@ -182,12 +181,13 @@ __device__ __forceinline__ void write_outputs(const Ta (&acc)[kD][K], const Dedi
         Ta *plane = reinterpret_cast<Ta *>(a.plane);
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            if (slot0 + d >= cnt) break;
-            Ta *orow = plane + (size_t)(first + slot0 + d) * (size_t)a.ld_plane;
+            if (slot0 + d < cnt) {
+                Ta *orow = plane + (size_t)(first + slot0 + d) * (size_t)a.ld_plane;
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int t = sample(k);
-                if (t < n) orow[t] = acc[d][k];
+                for (int k = 0; k < K; ++k) {
+                    const int t = sample(k);
+                    if (t < n) orow[t] = acc[d][k];
+                }
             }
         }
     }
@@ -196,7 +196,7 @@ __device__ __forceinline__ void write_outputs(const Ta (&acc)[kD][K], const Dedi
         // accumulation type (few terms), then float64 wave reductions.
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            if (slot0 + d >= cnt) break;
+            if (slot0 + d >= cnt) continue;
             const Ta kt = __shfl(acc[d][0], 0, 64);
             Ta mx[4], s1[4], s2[4];
 #pragma unroll
@@ -417,7 +417,7 @@ dedisp_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const int32_
     }
     if (!active) return;
 
-    write_outputs<Tl, Ta, K, PLANE, STATS>(acc, a, first, slot0, cnt, t0, tt, lane);
+    write_outputs<Tl, Ta, K, kD, PLANE, STATS>(acc, a, first, slot0, cnt, t0, tt, lane);
 }
 
 
@@ -426,74 +426,132 @@ dedisp_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const int32_
 //
 // Channels are taken in groups of G adjacent channels.  For trial d and group g the
 // shifts are s_{d,c0+k} = b_d + v_k, with b_d the group's first-channel shift and v the
-// group's relative-shift VECTOR.  Adjacent plan trials share v (a group's channels drift
-// apart by ~G/nchan sample per trial), so the 64 trials of a DM tile need one or two
-// distinct vectors per group.  Per (DM tile, time tile) workgroup, stage by stage (a
-// stage = a few consecutive groups):
+// group's relative-shift VECTOR.  Plan trials share a handful of vectors per group
+// (channels of a group drift apart by ~G/nchan sample per trial; the floor() of each
+// channel's delay jitters by one), so a DM tile of 128 trials needs ~4 distinct vectors
+// per group.  Per (DM tile, time tile) workgroup, stage by stage (a stage = a few
+// consecutive groups):
 //   1. build: for every distinct vector v of the tile in the stage's groups -- a "slot"
 //      -- the exact partial sum  R[i] = sum_{k<G} x[c0+k][(t0 + lo + v_k + i) mod N]
 //      into LDS (two alignment copies: R[i] and R[i+1] at the same offset), from the
 //      stage's channel rows staged in LDS by DMA (f32) or straight from global memory
-//      (u8 / f64, converted to f32);
+//      (u8 / f64, converted to f32).  One slot per wave at a time, U 64-element chunks
+//      per pass with all their reads in flight;
 //   2. sum: every trial adds ONE window of its slot per group:
 //      out_d[t0 + i] += R_{v(d)}[i + b_d - lo].
 // The gathered elements are the reference's (circular shift-and-sum; u8 exact), with
-// G x fewer adds than channel mode and each channel row read from L2 once per tile.
+// G x fewer adds than channel mode.
+//
+// Lane l of a wave owns samples t0 + 2l + 128j + e (j < K/2, e < 2) of D trials.
 typedef int i32x2 __attribute__((ext_vector_type(2)));
-typedef unsigned int u32x8 __attribute__((ext_vector_type(8)));
 
-constexpr int kSWaves = 8;                // subband mode: waves per workgroup (2 WGs = 4 waves/SIMD)
-constexpr int kSThreads = kSWaves * 64;
-constexpr int kSTPT = kSWaves * kD;       // trials per tile
-constexpr size_t kSubLdsBudget = 80 * 1024;
+// Workgroup shapes: W waves x D trials per wave, K samples per lane (time tile 64 K).
+template <int W_, int D_, int K_>
+struct SubCfg {
+    static constexpr int W = W_, D = D_, K = K_, J = K_ / 2, TT = 64 * K_, T = W_ * D_, THREADS = 64 * W_;
+};
+using SubWide = SubCfg<16, 8, 8>;   // 128 trials x 512 samples, one workgroup per CU (160 KiB LDS)
+using SubPair = SubCfg<8, 16, 4>;   // 128 trials x 256 samples, two workgroups per CU (80 KiB each)
+enum SubShape { SUB_WIDE = 0, SUB_PAIR = 1 };
+
+// Slot record (int32): slot length (elements, <= TT + spread + 1), copy-0 byte offset in
+// the slot area, first channel, channels in the group, then the G sources of element
+// 0 (raw-row float offsets in LDS, or sample indices mod N before adding t0).  Padded
+// to a whole s_load.
+__host__ __device__ constexpr int slot_stride(int G) { return G <= 4 ? 8 : 16; }
 
 struct SubArgs {
     DedispArgs o;           // data, ld, nchan, n, ndt, ntt, small_n; plane / partials
     int32_t ngroups;
     int32_t raw_stride;     // floats per staged channel row (DMA mode)
-    int32_t slot_area;      // LDS byte offset of the slot area
+    int32_t slot_area;      // LDS byte offset of the slot area (after the raw rows)
+    int32_t zero_row;       // LDS byte offset of a zero row (DMA mode), up to slot_area
+    int32_t skip;           // tuning ablation (PU_SUB_SKIP; results invalid): 1 build, 2 sum, 4 DMA
 };
 
-// Counted LDS wait that also "defines" the window registers it guards, so the adds
+// Counted LDS wait that also "defines" the J window registers it guards, so the adds
 // that read them cannot be hoisted above it.  lgkmcnt counts the inline-asm reads in
-// issue order; an outstanding scalar load only makes the wait longer, never shorter.
-template <int N>
-__device__ __forceinline__ void wait_lgkm(double (&w)[4])
+// issue order; an LDS op issued earlier or an outstanding scalar load only makes the
+// wait longer, never shorter.
+#define PU_WAIT_CASE(N)                                                                        \
+    if constexpr (J == 4)                                                                      \
+        asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]) \
+                     : : "memory");                                                            \
+    else                                                                                       \
+        asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(w[0]), "+v"(w[1]) : : "memory");
+
+template <int J, int N>
+__device__ __forceinline__ void wait_window_n(double (&w)[J])
 {
-    static_assert(N == 0 || N == 4 || N == 8 || N == 12, "lgkmcnt");
-    if constexpr (N == 12)
-        asm volatile("s_waitcnt lgkmcnt(12)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]) : : "memory");
-    else if constexpr (N == 8)
-        asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]) : : "memory");
-    else if constexpr (N == 4)
-        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]) : : "memory");
+    static_assert(J == 2 || J == 4, "window reads");
+    static_assert(N % J == 0 && N <= 3 * J, "lgkmcnt");
+    if constexpr (N == 12) {
+        PU_WAIT_CASE(12)
+    } else if constexpr (N == 8) {
+        PU_WAIT_CASE(8)
+    } else if constexpr (N == 6) {
+        PU_WAIT_CASE(6)
+    } else if constexpr (N == 4) {
+        PU_WAIT_CASE(4)
+    } else if constexpr (N == 2) {
+        PU_WAIT_CASE(2)
+    } else {
+        PU_WAIT_CASE(0)
+    }
+}
+#undef PU_WAIT_CASE
+
+// J x ds_read_b64 of one window (no wait).  Inline asm: hipcc would merge pairs into
+// ds_read2st64_b64, which runs at half the LDS rate.
+template <int J>
+__device__ __forceinline__ void issue_window(double (&w)[J], uint32_t addr)
+{
+    if constexpr (J == 4)
+        asm volatile(
+            "ds_read_b64 %0, %4\n\t"
+            "ds_read_b64 %1, %4 offset:512\n\t"
+            "ds_read_b64 %2, %4 offset:1024\n\t"
+            "ds_read_b64 %3, %4 offset:1536"
+            : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3])
+            : "v"(addr)
+            : "memory");
     else
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]) : : "memory");
+        asm volatile(
+            "ds_read_b64 %0, %2\n\t"
+            "ds_read_b64 %1, %2 offset:512"
+            : "=&v"(w[0]), "=&v"(w[1])
+            : "v"(addr)
+            : "memory");
 }
 
 // One group's contribution to the wave's D trials: rec[d] = LDS byte offset (slot area
-// relative) of trial d's window.  Every trial reads its window (4 x ds_read_b64 in
-// inline asm: hipcc would merge them into ds_read2st64_b64, half the LDS rate), three
-// trials ahead of the adds, with counted waits.
-__device__ __forceinline__ void group_trials(float (&acc)[kD][8], const u32x8 rec, uint32_t base)
+// relative) of trial d's window; reads run 3 trials ahead of the adds.
+template <class C, typename RecT>
+__device__ __forceinline__ void group_trials(float (&acc)[C::D][C::K], const RecT rec, uint32_t base)
 {
-    double w[4][4];
-    prefetch_window(w[0], base + rec[0]);
-    prefetch_window(w[1], base + rec[1]);
-    prefetch_window(w[2], base + rec[2]);
+    constexpr int D = C::D, J = C::J;
+    double w[4][J];
+    issue_window<J>(w[0], base + rec[0]);
+    issue_window<J>(w[1], base + rec[1]);
+    issue_window<J>(w[2], base + rec[2]);
 #pragma unroll
-    for (int d = 0; d < kD; ++d) {
-        if (d + 3 < kD) prefetch_window(w[(d + 3) & 3], base + rec[d + 3]);
-        constexpr int kAhead[kD] = {3, 3, 3, 3, 3, 2, 1, 0};
-        double(&wd)[4] = w[d & 3];
-        switch (kAhead[d]) {
-        case 3: wait_lgkm<12>(wd); break;
-        case 2: wait_lgkm<8>(wd); break;
-        case 1: wait_lgkm<4>(wd); break;
-        default: wait_lgkm<0>(wd); break;
+    for (int d = 0; d < D; ++d) {
+        if (d + 3 < D) issue_window<J>(w[(d + 3) & 3], base + rec[d + 3]);
+        double(&wd)[J] = w[d & 3];
+        const int ahead = D - 1 - d < 3 ? D - 1 - d : 3;
+        if (ahead == 3)
+            wait_window_n<J, 3 * J>(wd);
+        else if (ahead == 2)
+            wait_window_n<J, 2 * J>(wd);
+        else if (ahead == 1)
+            wait_window_n<J, J>(wd);
+        else
+            wait_window_n<J, 0>(wd);
+#pragma unroll
+        for (int k = 0; k < C::K; ++k) {
+            const uint64_t bits = __builtin_bit_cast(uint64_t, wd[k >> 1]);
+            acc[d][k] += __builtin_bit_cast(float, (uint32_t)((k & 1) ? (bits >> 32) : bits));
         }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc[d][k] += window_elem<float>(wd, k);
         pin_accumulators(acc[d]);
     }
 }
@@ -527,23 +585,19 @@ __device__ __forceinline__ void dma_row_f32(unsigned char *dst, const float *row
     }
 }
 
-// Slot record stride (int32): len, dst, gs, c0, G sources, padded to a whole s_load.
-__host__ __device__ constexpr int slot_meta_stride(int G) { return G <= 4 ? 8 : 16; }
-
-template <typename Tin, int G, bool PLANE, bool STATS>
-__global__ void __launch_bounds__(kSThreads, 4)
+template <class C, typename Tin, int G, bool PLANE, bool STATS>
+__global__ void __launch_bounds__(C::THREADS, 4)
 dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__restrict__ tile_stages,
                   const i32x4 *__restrict__ stages, const int32_t *__restrict__ slots,
-                  const int32_t *__restrict__ base_tab, const u32x8 *__restrict__ rec_tab)
+                  const int32_t *__restrict__ base_tab, const uint32_t *__restrict__ rec_tab)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr bool kDma = std::is_same<Tin, float>::value;
-    constexpr int K = 8;
-    constexpr int TT = 64 * K;
-    constexpr int D = kD;
-    constexpr int MS = slot_meta_stride(G);
-    constexpr int U = 4;  // build: elements per lane per pass (independent reads in flight)
+    constexpr int W = C::W, D = C::D, K = C::K, TT = C::TT;
+    constexpr int MS = slot_stride(G);
+    constexpr int U = ((TT + 80 + 63) / 64 + 1) / 2;  // chunks per build pass (two at a plan grid's spread)
     typedef int32_t meta_t __attribute__((ext_vector_type(MS)));
+    typedef uint32_t rec_t __attribute__((ext_vector_type(D)));
     const DedispArgs &o = a.o;
     const int ndt = o.ndt;
     const int wg = pu::xcd_remap(blockIdx.x, gridDim.x);
@@ -572,74 +626,83 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
 #pragma unroll
         for (int k = 0; k < K; ++k) acc[d][k] = 0.0f;
 
-    const u32x8 *recs = rec_tab + (size_t)dt * a.ngroups * kSWaves + wave;
+    const rec_t *recs = reinterpret_cast<const rec_t *>(rec_tab) + (size_t)dt * a.ngroups * W + wave;
+    if constexpr (kDma) {
+        // zero row (partial groups' missing channels) between the raw rows and the slots
+        float *zero = reinterpret_cast<float *>(smem + a.zero_row);
+        for (int i = tid; i < (a.slot_area - a.zero_row) / 4; i += C::THREADS) zero[i] = 0.0f;
+    }
 
-    // ---- DMA mode: the channel rows of stage k into the raw area (one buffer)
+    // ---- DMA mode: the channel rows of stage k into the raw area
     auto issue_raw = [&](int k) {
         const i32x4 st = ld_uniform(stages + ts.x + k);  // {group begin, group end, slot begin, slot end}
         const int c0 = st.x * G;
         const int nc = min(st.y * G, o.nchan) - c0;
         const int cover_bytes = (tile.z * 4 + 255) & ~255;
         const int32_t *base = base_tab + (size_t)dt * o.nchan;
-        for (int ci = wave; ci < nc; ci += kSWaves) {
+        for (int ci = wave; ci < nc; ci += W) {
             const int c = c0 + ci;
             int start = ld_uniform(base + c) + t0;
             if (start >= n) start -= n;
-            dma_row_f32(smem + (size_t)ci * a.raw_stride * 4,
+            dma_row_f32(smem + ci * a.raw_stride * 4,
                         reinterpret_cast<const float *>(data) + (size_t)c * (size_t)o.ld, start, cover_bytes, n,
                         small_n, lane);
         }
     };
 
-    // ---- build the stage's slots, one slot per wave at a time: R[i] (i < len) at
-    // copy 0 [i] and copy 1 [i - 1]; U elements per lane per pass, all reads first
-    auto build = [&](const i32x4 st) {
-        auto load = [&](const meta_t &m, int q, int i) -> float {
-            if constexpr (kDma) {
-                return raw_lds[m[4 + q] + i];
+    auto load = [&](const meta_t &m, int q, int i) -> float {
+        if constexpr (kDma) {
+            return raw_lds[m[4 + q] + i];  // past the slot only for masked lanes (row padding)
+        } else {
+            int pos = m[4 + q] + t0 + i;
+            if (small_n) {
+                pos %= n;
             } else {
-                int pos = m[4 + q] + t0 + i;
-                if (small_n) {
-                    pos %= n;
-                } else {
-                    if (pos >= n) pos -= n;
-                    if (pos >= n) pos -= n;
-                }
-                return static_cast<float>(data[(size_t)(m[3] + q) * (size_t)o.ld + pos]);
+                if (pos >= n) pos -= n;
+                if (pos >= n) pos -= n;
             }
-        };
-        for (int s = st.z + wave; s < st.w; s += kSWaves) {
+            const int ch = min(m[2] + q, o.nchan - 1);  // partial groups: in-bounds, discarded
+            return static_cast<float>(data[(size_t)ch * (size_t)o.ld + pos]);
+        }
+    };
+
+    // ---- build the stage's slots, one per wave at a time: R[i] (i < len) at copy 0 [i]
+    // and copy 1 [i - 1]; U chunks of 64 per pass, all G x U reads in flight
+    auto build = [&](const i32x4 st) {
+        for (int s = st.z + wave; s < st.w; s += W) {
             const meta_t m = ld_uniform(reinterpret_cast<const meta_t *>(slots + (size_t)s * MS));
-            const int len = m[0], gs = m[2];
+            const int len = m[0], gs = m[3];
             float *out0 = slot_lds + m[1] / 4;
             float *out1 = out0 + copy_bytes / 4 - 1;  // out1[0] lands in copy 0's padding
             for (int i0 = 0; i0 < len; i0 += 64 * U) {
-                int idx[U];
+                float v[U][G];
+                if (kDma || gs == G) {  // branch-free, all G x U reads in flight (DMA mode: a
+                                        // partial group's missing channels read the zero row)
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+#pragma unroll
+                        for (int q = 0; q < G; ++q) v[u][q] = load(m, q, i0 + 64 * u + lane);
+                } else {        // the last, partial group of a band
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+#pragma unroll
+                        for (int q = 0; q < G; ++q) v[u][q] = q < gs ? load(m, q, i0 + 64 * u + lane) : 0.0f;
+                }
                 float r[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    idx[u] = min(i0 + 64 * u + lane, len - 1);  // clamped: reads stay branch-free
                     r[u] = 0.0f;
+#pragma unroll
+                    for (int q = 0; q < G; ++q) r[u] += v[u][q];
                 }
-                if (gs == G) {
-                    float v[G][U];
+                // all sums before the first (chunk-uniform) write branch: keeps every read
+                // of the pass in flight together
 #pragma unroll
-                    for (int q = 0; q < G; ++q)
-#pragma unroll
-                        for (int u = 0; u < U; ++u) v[q][u] = load(m, q, idx[u]);
-#pragma unroll
-                    for (int q = 0; q < G; ++q)
-#pragma unroll
-                        for (int u = 0; u < U; ++u) r[u] += v[q][u];
-                } else {
-                    for (int q = 0; q < gs; ++q)
-#pragma unroll
-                        for (int u = 0; u < U; ++u) r[u] += load(m, q, idx[u]);
-                }
+                for (int u = 0; u < U; ++u) asm volatile("" : "+v"(r[u]));
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    const int i = i0 + 64 * u + lane;
-                    if (i < len) {
+                    if (i0 + 64 * u < len) {  // whole chunks: lanes past len write row padding
+                        const int i = i0 + 64 * u + lane;
                         out0[i] = r[u];
                         out1[i] = r[u];
                     }
@@ -652,22 +715,22 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
     for (int k = 0; k < ts.y; ++k) {
         const i32x4 st = ld_uniform(stages + ts.x + k);
         __syncthreads();  // raw rows of stage k landed (vmcnt); every wave left the slot area
-        build(st);
+        if (!(a.skip & 1)) build(st);
         __syncthreads();  // slots built; every wave left the raw rows
         if constexpr (kDma) {
-            if (k + 1 < ts.y) issue_raw(k + 1);  // lands while this stage is summed
+            if (k + 1 < ts.y && !(a.skip & 4)) issue_raw(k + 1);  // lands while this stage is summed
         }
-        if (!active) continue;
+        if (!active || (a.skip & 2)) continue;
         const uint32_t sb = smem_addr + (uint32_t)a.slot_area + 8u * lane;
-        u32x8 rec = ld_uniform(recs + (size_t)st.x * kSWaves);
+        rec_t rec = ld_uniform(recs + (size_t)st.x * W);
         for (int g = st.x; g < st.y; ++g) {
-            const u32x8 next = g + 1 < st.y ? ld_uniform(recs + (size_t)(g + 1) * kSWaves) : rec;
-            group_trials(acc, rec, sb);
+            const rec_t next = g + 1 < st.y ? ld_uniform(recs + (size_t)(g + 1) * W) : rec;
+            group_trials<C>(acc, rec, sb);
             rec = next;
         }
     }
     if (!active) return;
-    write_outputs<float, float, K, PLANE, STATS>(acc, o, first, slot0, cnt, t0, tt, lane);
+    write_outputs<float, float, K, D, PLANE, STATS>(acc, o, first, slot0, cnt, t0, tt, lane);
 }
 
 // One workgroup per trial: combine the per-time-tile partials in a fixed order
@@ -779,14 +842,14 @@ struct pu_plan {
     int32_t *d_first = nullptr, *d_count = nullptr, *d_rowlen = nullptr, *d_base = nullptr;
     u32x4 *d_rec = nullptr;
     // subband mode (group > 1): per tile {first, count, raw row length, copy bytes},
-    // stages {group begin, group end, slot begin, slot end}, slot records, window records
-    int group = 1, ngroups = 0, nslots_total = 0, raw_stride = 0;
-    size_t slot_area = 0;
+    // stages {group begin, group end, item begin, item end}, build items, window records
+    int group = 1, ngroups = 0, nslots_total = 0, raw_stride = 0, shape = SUB_WIDE;
+    size_t slot_area = 0, slot_bytes = 0, zero_row = 0;
     int64_t nstages = 0;
     i32x4 *d_tiles = nullptr, *d_stages = nullptr;
     i32x2 *d_tile_stages = nullptr;
     int32_t *d_slots = nullptr;
-    u32x8 *d_rec8 = nullptr;
+    uint32_t *d_recs = nullptr;
     // optional kernel timing: events before the first and after the last launch of
     // each dispatch
     std::vector<hipEvent_t> ev_start, ev_stop;
@@ -838,7 +901,7 @@ int dispatch_variant(const pu_plan *p, const DedispArgs &a, bool plane, hipStrea
     return PU_EINVAL;
 }
 
-template <typename Tin, int G>
+template <class C, typename Tin, int G>
 int launch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
 {
     SubArgs sa{};
@@ -846,41 +909,49 @@ int launch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
     sa.ngroups = p->ngroups;
     sa.raw_stride = p->raw_stride;
     sa.slot_area = (int32_t)p->slot_area;
-    const dim3 grid((unsigned)((int64_t)p->ndt * p->ntt)), block(kSThreads);
+    sa.zero_row = (int32_t)p->zero_row;
+    if (const char *env = getenv("PU_SUB_SKIP")) sa.skip = atoi(env);
+    const dim3 grid((unsigned)((int64_t)p->ndt * p->ntt)), block(C::THREADS);
     if (plane) {
-        auto kern = dedisp_sub_kernel<Tin, G, true, false>;
+        auto kern = dedisp_sub_kernel<C, Tin, G, true, false>;
         int rc = ensure_lds(kern, p->lds_bytes);
         if (rc) return rc;
         hipLaunchKernelGGL(kern, grid, block, p->lds_bytes, s, sa, p->d_tiles, p->d_tile_stages, p->d_stages,
-                           p->d_slots, p->d_base, p->d_rec8);
+                           p->d_slots, p->d_base, p->d_recs);
     } else {
-        auto kern = dedisp_sub_kernel<Tin, G, false, true>;
+        auto kern = dedisp_sub_kernel<C, Tin, G, false, true>;
         int rc = ensure_lds(kern, p->lds_bytes);
         if (rc) return rc;
         hipLaunchKernelGGL(kern, grid, block, p->lds_bytes, s, sa, p->d_tiles, p->d_tile_stages, p->d_stages,
-                           p->d_slots, p->d_base, p->d_rec8);
+                           p->d_slots, p->d_base, p->d_recs);
     }
     return pu::launch_check("dedisp_sub_kernel");
 }
 
-template <typename Tin>
+template <class C, typename Tin>
 int launch_sub_g(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
 {
     switch (p->group) {
-    case 2: return launch_sub<Tin, 2>(p, a, plane, s);
-    case 4: return launch_sub<Tin, 4>(p, a, plane, s);
-    case 8: return launch_sub<Tin, 8>(p, a, plane, s);
+    case 2: return launch_sub<C, Tin, 2>(p, a, plane, s);
+    case 4: return launch_sub<C, Tin, 4>(p, a, plane, s);
+    case 8: return launch_sub<C, Tin, 8>(p, a, plane, s);
     }
     pu::set_error("bad plan group %d", p->group);
     return PU_EINVAL;
 }
 
+template <typename Tin>
+int launch_sub_shape(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
+{
+    return p->shape == SUB_PAIR ? launch_sub_g<SubPair, Tin>(p, a, plane, s) : launch_sub_g<SubWide, Tin>(p, a, plane, s);
+}
+
 int dispatch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
 {
     switch (p->dtype) {
-    case PU_U8: return launch_sub_g<uint8_t>(p, a, plane, s);
-    case PU_F32: return launch_sub_g<float>(p, a, plane, s);
-    case PU_F64: return launch_sub_g<double>(p, a, plane, s);
+    case PU_U8: return launch_sub_shape<uint8_t>(p, a, plane, s);
+    case PU_F32: return launch_sub_shape<float>(p, a, plane, s);
+    case PU_F64: return launch_sub_shape<double>(p, a, plane, s);
     }
     pu::set_error("bad plan dtype");
     return PU_EINVAL;
@@ -919,7 +990,7 @@ void free_plan(pu_plan *p)
     (void)hipFree(p->d_tile_stages);
     (void)hipFree(p->d_stages);
     (void)hipFree(p->d_slots);
-    (void)hipFree(p->d_rec8);
+    (void)hipFree(p->d_recs);
     delete p;
 }
 
@@ -1052,20 +1123,23 @@ struct SubSlot {
     int64_t d0;      // one trial with this vector
 };
 
-int plan_sub(pu_plan *p, const int64_t *shifts, int G, size_t budget)
+int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
 {
     const int64_t nchan = p->nchan, n = p->n, ndm = p->ndm;
-    const int64_t TT = p->TT;
+    const int W = shape == SUB_PAIR ? SubPair::W : SubWide::W;
+    const int D = shape == SUB_PAIR ? SubPair::D : SubWide::D;
+    const int64_t TT = shape == SUB_PAIR ? SubPair::TT : SubWide::TT;
+    const int64_t T = (int64_t)W * D;
     const int ngroups = (int)((nchan + G - 1) / G);
     const bool dma = p->dtype == PU_F32;
-    const int64_t raw_cap = dma ? (int64_t)budget / 2 : 0;
+    // raw rows (DMA mode) and slots share the budget; a stage holds whole groups
+    const int64_t raw_cap = dma ? (int64_t)budget * 3 / 10 : 0;
     const int64_t slot_cap = (int64_t)budget - raw_cap;
     auto S = [&](int64_t d, int64_t c) { return shifts[d * nchan + c]; };
     auto raw_stride_of = [&](int64_t spread) { return (TT + spread + 1 + 63) / 64 * 64; };
-    // slot copy: len = TT + span + 1 elements, + 1 padding float (build writes copy 1's
-    // element -1 there)
+    // slot copy: len = TT + span + 1 elements + 1 padding float (copy 1's element -1)
     auto copy_of = [&](int64_t span) { return (TT + span + 2 + 63) / 64 * 64 * 4; };
-    if (dma && G * raw_stride_of(0) * 4 > raw_cap) return PU_EUNSUPPORTED;
+    if (dma && ((G + 1) * raw_stride_of(0) + 64) * 4 > raw_cap) return PU_EUNSUPPORTED;
     if (2 * copy_of(0) > slot_cap) return PU_EUNSUPPORTED;
 
     // ---- relative-shift vector id per (trial, group): v_k = s[c0 + k] - s[c0], k < gs
@@ -1095,7 +1169,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, size_t budget)
         }
     }
 
-    // ---- DM tiles: <= kSTPT consecutive trials whose channel rows (one group's worth)
+    // ---- DM tiles: <= T consecutive trials whose channel rows (one group's worth)
     // fit the raw area and whose slots of any one group fit the slot area
     std::vector<int32_t> first, count;
     std::vector<int64_t> spread_t, span_t, smin_t;  // smin_t: per tile x channel
@@ -1112,12 +1186,12 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, size_t budget)
             }
             int64_t spread = 0, span = 0;
             int64_t j = i + 1;
-            while (j < ndm && j - i < kSTPT) {
+            while (j < ndm && j - i < T) {
                 int64_t sp = spread;
                 for (int64_t c = 0; c < nchan; ++c)
                     sp = std::max(sp, std::max(mx[c], S(j, c)) - std::min(mn[c], S(j, c)));
                 if (sp > kSubMaxSpread) break;
-                if (dma && G * raw_stride_of(sp) * 4 > raw_cap) break;
+                if (dma && ((G + 1) * raw_stride_of(sp) + 64) * 4 > raw_cap) break;
                 int64_t spn = span;
                 size_t maxslots = 0;
                 for (int g = 0; g < ngroups; ++g) {
@@ -1162,15 +1236,19 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, size_t budget)
         max_spread = std::max(max_spread, spread_t[t]);
     }
     // channels one stage may stage (>= G: the widest tile passed G * its stride <= raw_cap)
-    const int64_t chan_cap = dma ? raw_cap / (raw_stride * 4) : (int64_t)INT32_MAX;
+    const int64_t chan_cap = dma ? (raw_cap / 4 - raw_stride - 64) / raw_stride : (int64_t)INT32_MAX;
+    if (dma && chan_cap < G) return PU_EUNSUPPORTED;
 
     // ---- stages (consecutive groups whose channels and slots fit), slot records, window
-    // records, DMA row bases
-    const int ms = slot_meta_stride(G);
+    // records (D per wave and group), DMA row bases.  DMA mode: a zero row of raw_stride
+    // + 64 floats follows the largest stage's rows (the G - gs missing channels of a
+    // partial group read it, so the build never branches on the group size).
+    const int ms = slot_stride(G);
+    const int64_t zero_row_f = chan_cap * raw_stride;  // float offset; the raw area is sized below
     std::vector<i32x4> tiles((size_t)ndt), stages;
     std::vector<i32x2> tile_stages((size_t)ndt);
     std::vector<int32_t> slotmeta, base;
-    std::vector<u32x8> rec((size_t)ndt * ngroups * kSWaves);
+    std::vector<uint32_t> rec((size_t)ndt * ngroups * W * D);
     std::vector<int64_t> slot_local((size_t)ngroups);
     int64_t slot_used = 0, max_stage_chans = 0;
     for (int t = 0; t < ndt; ++t) {
@@ -1198,10 +1276,10 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, size_t budget)
                 for (const auto &sl : sls) {
                     slotmeta.push_back((int32_t)(TT + (sl.hi - sl.lo) + 1));
                     slotmeta.push_back((int32_t)(used * 2 * cb));
-                    slotmeta.push_back(gs);
                     slotmeta.push_back((int32_t)c0);
+                    slotmeta.push_back(gs);
                     for (int k = 0; k < ms - 4; ++k) {
-                        int64_t src = 0;
+                        int64_t src = dma && k < G ? zero_row_f : 0;  // missing channel: zero row
                         if (k < gs) {
                             // smallest shift of channel c0+k over the slot's trials
                             const int64_t sk = sl.lo + S(sl.d0, c0 + k) - S(sl.d0, c0);
@@ -1227,38 +1305,44 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, size_t budget)
         }
         for (int gg = 0; gg < ngroups; ++gg) {
             const auto &sls = tslots[(size_t)t * ngroups + gg];
-            for (int w = 0; w < kSWaves; ++w) {
-                u32x8 r;
-                for (int d = 0; d < kD; ++d) {
-                    const int64_t tr = first[t] + std::min(w * kD + d, count[t] - 1);  // padding repeats the last trial
+            for (int w = 0; w < W; ++w) {
+                uint32_t *r = rec.data() + (((size_t)t * ngroups + gg) * W + w) * D;
+                for (int d = 0; d < D; ++d) {
+                    const int64_t tr = first[t] + std::min<int64_t>(w * D + d, count[t] - 1);  // padding repeats the last trial
                     const int32_t v = vid[(size_t)tr * ngroups + gg];
                     size_t si = 0;
                     while (sls[si].vid != v) ++si;
                     const int64_t rr = S(tr, (int64_t)gg * G) - sls[si].lo;
                     r[d] = (uint32_t)((slot_local[gg] + (int64_t)si) * 2 * cb + (rr & 1) * cb + (rr & ~int64_t(1)) * 4);
                 }
-                rec[((size_t)t * ngroups + gg) * kSWaves + w] = r;
             }
         }
     }
-    const int64_t raw_used = dma ? (max_stage_chans * raw_stride * 4 + 255) / 256 * 256 : 0;
+    const int64_t raw_used = dma ? ((chan_cap * raw_stride + raw_stride + 64) * 4 + 255) / 256 * 256 : 0;
     if (raw_used + slot_used > 160 * 1024) {
         pu::set_error("subband mode: %lld bytes of LDS", (long long)(raw_used + slot_used));
         return PU_EUNSUPPORTED;
     }
-    if ((int64_t)ndt * p->ntt >= (int64_t(1) << 31) || (int64_t)slotmeta.size() >= (int64_t(1) << 31)) {
+    const int64_t ntt = (n + TT - 1) / TT;
+    if ((int64_t)ndt * ntt >= (int64_t(1) << 31) || (int64_t)slotmeta.size() >= (int64_t(1) << 31)) {
         pu::set_error("pu_plan_create: grid too large");
         return PU_EINVAL;
     }
     p->group = G;
     p->ngroups = ngroups;
     p->ndt = ndt;
+    p->shape = shape;
+    p->K = (int)(TT / 64);
+    p->TT = (int)TT;
+    p->ntt = (int)ntt;
     p->ncc = (int)max_stage_chans;
     p->raw_stride = (int)raw_stride;
     p->row_stride = (int)raw_stride;
     p->max_spread = (int)max_spread;
     p->small_n = raw_stride + 2 > n ? 1 : 0;
     p->slot_area = (size_t)raw_used;
+    p->zero_row = dma ? (size_t)(zero_row_f * 4) : (size_t)raw_used;
+    p->slot_bytes = (size_t)slot_used;
     p->lds_bytes = (size_t)(raw_used + slot_used);
     p->nslots_total = (int)(slotmeta.size() / ms);
     p->nstages = (int64_t)stages.size();
@@ -1267,7 +1351,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, size_t budget)
     if (!rc) rc = upload(&p->d_tile_stages, tile_stages);
     if (!rc) rc = upload(&p->d_stages, stages);
     if (!rc) rc = upload(&p->d_slots, slotmeta);
-    if (!rc) rc = upload(&p->d_rec8, rec);
+    if (!rc) rc = upload(&p->d_recs, rec);
     if (!rc && dma) rc = upload(&p->d_base, base);
     return rc;
 }
@@ -1293,7 +1377,7 @@ void reset_tables(pu_plan *p)
     (void)hipFree(p->d_tile_stages);
     (void)hipFree(p->d_stages);
     (void)hipFree(p->d_slots);
-    (void)hipFree(p->d_rec8);
+    (void)hipFree(p->d_recs);
     *p = keep;
 }
 
@@ -1332,7 +1416,10 @@ int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int
     p->ntt = (int)((n + p->TT - 1) / p->TT);
 
     // LDS budget per workgroup (channel / subband mode); PU_LDS_BUDGET_KB overrides (tuning)
-    size_t budget = kLdsBudget, sub_budget = kSubLdsBudget;
+    // subband workgroup shape: PU_SUB_SHAPE 0 = wide (1 WG/CU), 1 = pair (2 WGs/CU)
+    int shape = SUB_WIDE;
+    if (const char *env = getenv("PU_SUB_SHAPE")) shape = atoi(env) == 1 ? SUB_PAIR : SUB_WIDE;
+    size_t budget = kLdsBudget, sub_budget = shape == SUB_PAIR ? 80 * 1024 : 160 * 1024;
     if (const char *env = getenv("PU_LDS_BUDGET_KB")) budget = sub_budget = (size_t)std::max(8, atoi(env)) * 1024;
     // group size: explicit, else PU_GROUP, else 4; float32 accumulation only (the
     // float64 modes keep the reference's sequential channel order)
@@ -1346,7 +1433,7 @@ int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int
     while (G > 1 && G >= nchan) G >>= 1;
     int rc = PU_EUNSUPPORTED;
     for (; G > 1 && rc == PU_EUNSUPPORTED; G >>= 1) {
-        rc = plan_sub(p, shifts, G, sub_budget);
+        rc = plan_sub(p, shifts, G, shape, sub_budget);
         if (rc == PU_EUNSUPPORTED) reset_tables(p);
     }
     if (rc == PU_EUNSUPPORTED) rc = plan_channels(p, shifts, budget);
@@ -1398,9 +1485,9 @@ size_t pu_plan_workspace_bytes(const pu_plan *p)
 int pu_plan_info(const pu_plan *p, int64_t *info, int n)
 {
     if (!p || !info) return 0;
-    const int64_t v[] = {p->ndm, p->ndt, p->ntt, p->group > 1 ? kSTPT : kTPT, p->TT, p->ncc,
+    const int64_t v[] = {p->ndm, p->ndt, p->ntt, p->group > 1 ? (p->shape == SUB_PAIR ? SubPair::T : SubWide::T) : kTPT, p->TT, p->ncc,
                          p->row_stride, (int64_t)p->lds_bytes, kVariants[p->variant].acc_f64, p->max_spread,
-                         p->group, p->nslots_total, p->nstages, (int64_t)p->slot_area, p->raw_stride};
+                         p->group, p->nslots_total, p->nstages, (int64_t)p->slot_bytes, p->raw_stride};
     const int m = std::min<int>(n, (int)(sizeof v / sizeof v[0]));
     for (int k = 0; k < m; ++k) info[k] = v[k];
     return m;

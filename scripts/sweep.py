@@ -1,8 +1,9 @@
 """Interleaved A/B of dedispersion plan variants in ONE process (guide §5.4 rule 24).
 
 Usage: python scripts/sweep.py [config]
-  env PU_SWEEP="G:KB,..." selects (channel-group size, LDS budget KB) pairs,
-  e.g. "1:64,2:64,4:64,4:80,8:64" (group 1 = channel mode).  PU_ROUNDS rounds.
+  env PU_SWEEP="G:KB[:shape],..." selects (channel-group size, LDS budget KB, subband
+  workgroup shape 0 wide / 1 pair) variants, e.g. "1:64,4:160:0,4:80:1" (group 1 =
+  channel mode).  PU_ROUNDS rounds.
 Prints one line per (variant, round) and a median summary; the S/N of every trial
 is compared with the first variant's (float32 tolerance).
 """
@@ -27,10 +28,11 @@ if ntrials:
     dms = dms[:ntrials]
 sh = _hip.shift_table(cfg.nchan, dms, cfg.start_freq, cfg.bandwidth, cfg.tsamp)
 plans = {}
-for g, b in variants:
-    os.environ["PU_LDS_BUDGET_KB"] = str(b)
-    plans[(g, b)] = _hip.Plan(_hip.dtype_code(x.dtype), _hip.PU_ACC_NATIVE, cfg.nchan, cfg.nsamples, sh, group=g)
-    print("variant", (g, b), plans[(g, b)].info, flush=True)
+for v in variants:
+    os.environ["PU_LDS_BUDGET_KB"] = str(v[1])
+    os.environ["PU_SUB_SHAPE"] = str(v[2] if len(v) > 2 else 0)
+    plans[v] = _hip.Plan(_hip.dtype_code(x.dtype), _hip.PU_ACC_NATIVE, cfg.nchan, cfg.nsamples, sh, group=v[0])
+    print("variant", v, plans[v].info, flush=True)
 ws = torch.empty(max(p.workspace_bytes for p in plans.values()), dtype=torch.uint8, device=x.device)
 res = {v: [] for v in plans}
 ref = None
@@ -46,9 +48,9 @@ for r in range(rounds):
         if ref is None:
             ref = snr
         ok = np.allclose(snr, ref, rtol=1e-5)
-        print(f"round {r} group {v[0]} lds {v[1]}KB: {np.median(ms):.3f} ms same={ok}", flush=True)
+        print(f"round {r} variant {v}: {np.median(ms):.3f} ms same={ok}", flush=True)
 samples = cfg.nsamples * dms.size
 for v in plans:
     m = float(np.median(res[v]))
-    print(f"SUMMARY group {v[0]} lds {v[1]}KB median {m:.3f} ms  {samples / m * 1e3:.3e} samples/s  "
+    print(f"SUMMARY variant {v} median {m:.3f} ms  {samples / m * 1e3:.3e} samples/s  "
           f"brute-force-equivalent {cfg.nchan * samples / m / 1e9:.2f} Tadd/s")

@@ -165,7 +165,7 @@ def test_plane_subband_small_lds_budget(gpu, dt, monkeypatch):
     x = {"u8": x.astype(np.uint8), "f32": x.astype(np.float32), "f64": x}[dt]
     dms = np.linspace(c.dmmin, c.dmmax, 90)
     sh = _hip.shift_table(c.nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
-    monkeypatch.setenv("PU_LDS_BUDGET_KB", "24")
+    monkeypatch.setenv("PU_LDS_BUDGET_KB", "96")
     info = {}
     plane = _plane(x, sh, "f32" if dt == "f64" else "native", 4, info)
     assert info["group"] == 4 and info["stages"] > 2 * info["dm_tiles"], info
