@@ -65,18 +65,6 @@ struct DedispArgs {
     double *partials;
 };
 
-template <typename T>
-__device__ __forceinline__ T shfl_down(T v, int d)
-{
-    return __shfl_down(v, d, 64);
-}
-
-template <typename T>
-__device__ __forceinline__ T shfl_xor(T v, int d)
-{
-    return __shfl_xor(v, d, 64);
-}
-
 // Uniform (scalar-cache) load: the constant address space makes hipcc emit s_load.
 template <typename T>
 __device__ __forceinline__ T ld_uniform(const T *p)
@@ -164,6 +152,63 @@ __device__ __forceinline__ void channel_trials(Ta (&acc)[kD][K], double (&w)[4],
     }
 }
 
+// ---- DPP cross-lane helpers (gfx9 DPP: quad_perm / row_shl / row_ror / row_bcast).
+// VALU-only: unlike __shfl (ds_bpermute), they use no LDS bandwidth.
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t old, uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROW_MASK, 0xf, false);
+}
+
+template <int CTRL, int ROW_MASK = 0xf, typename T>
+__device__ __forceinline__ T dpp(T old, T v)
+{
+    if constexpr (sizeof(T) == 4) {
+        return __builtin_bit_cast(T, dpp_u32<CTRL, ROW_MASK>(__builtin_bit_cast(uint32_t, old),
+                                                             __builtin_bit_cast(uint32_t, v)));
+    } else {
+        const uint64_t o = __builtin_bit_cast(uint64_t, old), x = __builtin_bit_cast(uint64_t, v);
+        const uint64_t lo = dpp_u32<CTRL, ROW_MASK>((uint32_t)o, (uint32_t)x);
+        const uint64_t hi = dpp_u32<CTRL, ROW_MASK>((uint32_t)(o >> 32), (uint32_t)(x >> 32));
+        return __builtin_bit_cast(T, lo | (hi << 32));
+    }
+}
+
+// Value of lane l + S within the lane's row of 16 (row_shl:S); lanes past the row end
+// get 0.  Used only where l + S stays in the row.
+template <int S, typename T>
+__device__ __forceinline__ T row_down(T v)
+{
+    return dpp<0x100 + S>(T(0), v);
+}
+
+// Wave reductions to lane 63: within rows (quad xor 1, 2, row_ror 4, 8), then
+// row_bcast15 into rows 1 and 3, row_bcast31 into rows 2 and 3.
+template <typename T>
+__device__ __forceinline__ T wave_sum_to63(T v)
+{
+    v += dpp<0xB1>(T(0), v);
+    v += dpp<0x4E>(T(0), v);
+    v += dpp<0x124>(T(0), v);
+    v += dpp<0x128>(T(0), v);
+    v += dpp<0x142, 0xA>(T(0), v);
+    v += dpp<0x143, 0xC>(T(0), v);
+    return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_max_to63(T v)
+{
+    const T lo = -INFINITY;
+    v = fmax(v, dpp<0xB1>(lo, v));
+    v = fmax(v, dpp<0x4E>(lo, v));
+    v = fmax(v, dpp<0x124>(lo, v));
+    v = fmax(v, dpp<0x128>(lo, v));
+    v = fmax(v, dpp<0x142, 0xA>(lo, v));
+    v = fmax(v, dpp<0x143, 0xC>(lo, v));
+    return v;
+}
+
 // Outputs of one wave: the dedispersed plane rows of its D trials, or their per-tile
 // partial statistics (1/2/4/8-sample rebinned sums: max, shifted sum, shifted sum of
 // squares; lane-local in the accumulation type, then float64 wave reductions).
@@ -197,7 +242,14 @@ __device__ __forceinline__ void write_outputs(const Ta (&acc)[D][K], const Dedis
 #pragma unroll
         for (int d = 0; d < D; ++d) {
             if (slot0 + d >= cnt) continue;
-            const Ta kt = __shfl(acc[d][0], 0, 64);
+            Ta kt;  // lane 0's first sample: the shift that keeps the sums well conditioned
+            if constexpr (sizeof(Ta) == 4) {
+                kt = __builtin_bit_cast(Ta, __builtin_amdgcn_readlane(__builtin_bit_cast(int, acc[d][0]), 0));
+            } else {
+                const uint64_t b = __builtin_bit_cast(uint64_t, acc[d][0]);
+                kt = __builtin_bit_cast(Ta, (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, 0) |
+                                                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), 0) << 32));
+            }
             Ta mx[4], s1[4], s2[4];
 #pragma unroll
             for (int w = 0; w < 4; ++w) {
@@ -223,39 +275,35 @@ __device__ __forceinline__ void write_outputs(const Ta (&acc)[D][K], const Dedis
                     account(0, a1, t + 1, true);
                     Ta r = a0 + a1;                       // width 2, in-lane
                     account(1, r, t, true);
-                    r += shfl_down(r, 1);                 // width 4
+                    r += row_down<1>(r);                  // width 4
                     account(2, r, t, (lane & 1) == 0);
-                    r += shfl_down(r, 2);                 // width 8
+                    r += row_down<2>(r);                  // width 8
                     account(3, r, t, (lane & 3) == 0);
                 } else {
                     Ta r = acc[d][j];
                     const int t = sample(j);
                     account(0, r, t, true);
-#pragma unroll
-                    for (int w = 1; w < 4; ++w) {
-                        r += shfl_down(r, 1 << (w - 1));
-                        account(w, r, t, (lane & ((1 << w) - 1)) == 0);
-                    }
+                    r += row_down<1>(r);
+                    account(1, r, t, (lane & 1) == 0);
+                    r += row_down<2>(r);
+                    account(2, r, t, (lane & 3) == 0);
+                    r += row_down<4>(r);
+                    account(3, r, t, (lane & 7) == 0);
                 }
             }
             double* p = a.partials + ((size_t)(first + slot0 + d) * a.ntt + tt) * kPartStride;
 #pragma unroll
             for (int w = 0; w < 4; ++w) {
-                Ta m = mx[w];
-                double x1 = static_cast<double>(s1[w]), x2 = static_cast<double>(s2[w]);
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) {
-                    m = fmax(m, shfl_xor(m, off));
-                    x1 += shfl_xor(x1, off);
-                    x2 += shfl_xor(x2, off);
-                }
-                if (lane == 0) {
+                const Ta m = wave_max_to63(mx[w]);
+                const double x1 = wave_sum_to63(static_cast<double>(s1[w]));
+                const double x2 = wave_sum_to63(static_cast<double>(s2[w]));
+                if (lane == 63) {
                     p[1 + 3 * w] = static_cast<double>(m);
                     p[2 + 3 * w] = x1;
                     p[3 + 3 * w] = x2;
                 }
             }
-            if (lane == 0) p[0] = static_cast<double>(kt);
+            if (lane == 63) p[0] = static_cast<double>(kt);
         }
     }
 }
@@ -633,16 +681,16 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
         for (int i = tid; i < (a.slot_area - a.zero_row) / 4; i += C::THREADS) zero[i] = 0.0f;
     }
 
-    // ---- DMA mode: the channel rows of stage k into the raw area
-    auto issue_raw = [&](int k) {
-        const i32x4 st = ld_uniform(stages + ts.x + k);  // {group begin, group end, slot begin, slot end}
+    // ---- DMA mode: the channel rows of stage st into the raw area; base0 = this wave's
+    // first row base (prefetched)
+    const int32_t *base_t = base_tab + (size_t)dt * o.nchan;
+    auto issue_raw = [&](const i32x4 st, int base0) {
         const int c0 = st.x * G;
         const int nc = min(st.y * G, o.nchan) - c0;
         const int cover_bytes = (tile.z * 4 + 255) & ~255;
-        const int32_t *base = base_tab + (size_t)dt * o.nchan;
         for (int ci = wave; ci < nc; ci += W) {
             const int c = c0 + ci;
-            int start = ld_uniform(base + c) + t0;
+            int start = (ci == wave ? base0 : ld_uniform(base_t + c)) + t0;
             if (start >= n) start -= n;
             dma_row_f32(smem + ci * a.raw_stride * 4,
                         reinterpret_cast<const float *>(data) + (size_t)c * (size_t)o.ld, start, cover_bytes, n,
@@ -668,9 +716,9 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
 
     // ---- build the stage's slots, one per wave at a time: R[i] (i < len) at copy 0 [i]
     // and copy 1 [i - 1]; U chunks of 64 per pass, all G x U reads in flight
-    auto build = [&](const i32x4 st) {
+    auto build = [&](const i32x4 st, const meta_t m0) {
         for (int s = st.z + wave; s < st.w; s += W) {
-            const meta_t m = ld_uniform(reinterpret_cast<const meta_t *>(slots + (size_t)s * MS));
+            const meta_t m = s == st.z + wave ? m0 : ld_uniform(reinterpret_cast<const meta_t *>(slots + (size_t)s * MS));
             const int len = m[0], gs = m[3];
             float *out0 = slot_lds + m[1] / 4;
             float *out1 = out0 + copy_bytes / 4 - 1;  // out1[0] lands in copy 0's padding
@@ -711,25 +759,41 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
         }
     };
 
-    if constexpr (kDma) issue_raw(0);
-    for (int k = 0; k < ts.y; ++k) {
-        const i32x4 st = ld_uniform(stages + ts.x + k);
+    // ---- stage loop.  Scalar metadata is loaded one step ahead (the stage records of k+1
+    // and k+2, this wave's first DMA row base, slot record and window records), so the
+    // loads' latency overlaps the barrier waits instead of the phases.
+    const int ns = ts.y;
+    auto stage_at = [&](int k) { return ld_uniform(stages + ts.x + min(k, ns - 1)); };
+    auto base_of = [&](const i32x4 st) { return ld_uniform(base_t + min(st.x * G + wave, o.nchan - 1)); };
+    auto meta_of = [&](const i32x4 st) {
+        return ld_uniform(reinterpret_cast<const meta_t *>(slots + (size_t)min(st.z + wave, st.w - 1) * MS));
+    };
+    i32x4 st = stage_at(0), st1 = stage_at(1);
+    if constexpr (kDma) issue_raw(st, base_of(st));
+    for (int k = 0; k < ns; ++k) {
+        const i32x4 st2 = stage_at(k + 2);
+        const int b1 = kDma ? base_of(st1) : 0;
+        const meta_t m0 = meta_of(st);
+        const rec_t rec0 = ld_uniform(recs + (size_t)st.x * W);
         __syncthreads();  // raw rows of stage k landed (vmcnt); every wave left the slot area
-        if (!(a.skip & 1)) build(st);
+        if (!(a.skip & 1)) build(st, m0);
         __syncthreads();  // slots built; every wave left the raw rows
         if constexpr (kDma) {
-            if (k + 1 < ts.y && !(a.skip & 4)) issue_raw(k + 1);  // lands while this stage is summed
+            if (k + 1 < ns && !(a.skip & 4)) issue_raw(st1, b1);  // lands while this stage is summed
         }
-        if (!active || (a.skip & 2)) continue;
-        const uint32_t sb = smem_addr + (uint32_t)a.slot_area + 8u * lane;
-        rec_t rec = ld_uniform(recs + (size_t)st.x * W);
-        for (int g = st.x; g < st.y; ++g) {
-            const rec_t next = g + 1 < st.y ? ld_uniform(recs + (size_t)(g + 1) * W) : rec;
-            group_trials<C>(acc, rec, sb);
-            rec = next;
+        if (active && !(a.skip & 2)) {
+            const uint32_t sb = smem_addr + (uint32_t)a.slot_area + 8u * lane;
+            rec_t rec = rec0;
+            for (int g = st.x; g < st.y; ++g) {
+                const rec_t next = g + 1 < st.y ? ld_uniform(recs + (size_t)(g + 1) * W) : rec;
+                group_trials<C>(acc, rec, sb);
+                rec = next;
+            }
         }
+        st = st1;
+        st1 = st2;
     }
-    if (!active) return;
+    if (!active || (a.skip & 8)) return;
     write_outputs<float, float, K, D, PLANE, STATS>(acc, o, first, slot0, cnt, t0, tt, lane);
 }
 

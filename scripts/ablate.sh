@@ -1,7 +1,7 @@
 #!/bin/bash
 # Subband-kernel ablation: time the C2 plan with phases skipped (results invalid).
 cd "$GRAFT_REPO_ROOT"
-for sk in 0 1 2 3 4 7; do
+for sk in ${SKIPS:-0 1 2 3 4 7 8 15}; do
   echo "skip=$sk"
   PU_SUB_SKIP=$sk PU_ROUNDS=1 PU_SWEEP=${PU_SWEEP:-4:160:0} timeout -k 10 120 python3 scripts/sweep.py C2 2>&1 | grep SUMMARY || exit 1
 done
