@@ -37,6 +37,8 @@ HBM_PEAK_GBS = 8000.0
 # float32 vector peak is 157.3 TFLOP/s counting an FMA as 2 FLOP; an add is one FLOP
 # per lane-op, so the add-only ceiling is half of it: 256 CU x 128 lanes/clk x 2.4 GHz
 VALU_ADD_PEAK_TFLOPS = 78.6
+# LDS: 256 B/clk/CU for ds_read_b64 (MI355X_MICROARCH.md §LDS) x 256 CUs x 2.4 GHz
+LDS_PEAK_TBPS = 157.3
 
 
 def log(*a):
@@ -166,14 +168,25 @@ def main():
     alg_bytes = float(cfg.nchan) * cfg.nsamples * esz  # compulsory input read per launch (stats mode)
     roof = None
     if kernel_ms:
+        info = plan.info
         achieved = adds / (kernel_ms / 1e3) / 1e12
         roof = {"bound": "valu", "achieved": round(achieved, 3), "peak": VALU_ADD_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / VALU_ADD_PEAK_TFLOPS, 4),
                 "traffic": load_pmc(args.config),
-                "kernel": "dedisp_kernel", "kernel_ms": round(kernel_ms, 4),
+                "kernel": "dedisp_sub_kernel" if info["group"] > 1 else "dedisp_kernel",
+                "kernel_ms": round(kernel_ms, 4),
                 "algorithmic_flop_per_launch": adds, "algorithmic_bytes_per_launch": alg_bytes,
                 "hbm_compulsory_gbs": round(alg_bytes / (kernel_ms / 1e3) / 1e9, 1),
                 "hbm_compulsory_frac": round(alg_bytes / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+        if info["group"] > 1:
+            # executed work of the exact subband decomposition: G x fewer
+            # adds than the algorithm's; the LDS array (256 B/clk/CU) is its binding unit
+            lds = info["lds_traffic"] / (kernel_ms / 1e3) / 1e12
+            roof.update({"executed_flop_per_launch": info["exec_adds"],
+                         "executed_tflops": round(info["exec_adds"] / (kernel_ms / 1e3) / 1e12, 3),
+                         "lds_bytes_per_launch": info["lds_traffic"], "lds_achieved_TBps": round(lds, 2),
+                         "lds_peak_TBps": LDS_PEAK_TBPS, "lds_frac": round(lds / LDS_PEAK_TBPS, 4),
+                         "group": info["group"]})
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

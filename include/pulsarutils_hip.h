@@ -104,7 +104,9 @@ int pu_plan_kernel_times(pu_plan *plan, float *ms, int n);
 /* Introspection (tests / DESIGN.md): fills up to ``n`` of
  * {ndm, dm_tiles, time_tiles, trials_per_tile, time_tile, chans_per_step,
  *  row_stride, lds_bytes, acc_is_f64, max_spread, group, slots, stages,
- *  slot_bytes, raw_stride}. Returns the count written. */
+ *  slot_bytes, raw_stride, exec_adds, lds_traffic}: the last two are the adds and
+ *  LDS bytes (reads, writes, DMA) one launch executes (subband mode; 0 otherwise).
+ *  Returns the count written. */
 int pu_plan_info(const pu_plan *plan, int64_t *info, int n);
 
 /* ------------------------------------------------------------------ cleaning */

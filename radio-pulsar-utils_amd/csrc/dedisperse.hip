@@ -909,6 +909,7 @@ struct pu_plan {
     // stages {group begin, group end, item begin, item end}, build items, window records
     int group = 1, ngroups = 0, nslots_total = 0, raw_stride = 0, shape = SUB_WIDE;
     size_t slot_area = 0, slot_bytes = 0, zero_row = 0;
+    int64_t exec_adds = 0, lds_traffic = 0;  // per launch (measurement: bench.py roofline)
     int64_t nstages = 0;
     i32x4 *d_tiles = nullptr, *d_stages = nullptr;
     i32x2 *d_tile_stages = nullptr;
@@ -1167,6 +1168,7 @@ int plan_channels(pu_plan *p, const int64_t *shifts, size_t budget)
         pu::set_error("pu_plan_create: grid too large");
         return PU_EINVAL;
     }
+    p->exec_adds = ndm * nchan * (int64_t)p->ntt * p->TT;
     int rc = PU_OK;
     if (!rc) rc = upload(&p->d_first, first);
     if (!rc) rc = upload(&p->d_count, count);
@@ -1315,9 +1317,13 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     std::vector<uint32_t> rec((size_t)ndt * ngroups * W * D);
     std::vector<int64_t> slot_local((size_t)ngroups);
     int64_t slot_used = 0, max_stage_chans = 0;
+    int64_t adds_tile = 0, lds_tile = 0;  // per time tile, summed over DM tiles
     for (int t = 0; t < ndt; ++t) {
         const int64_t cb = copy_of(span_t[t]);
         const int64_t *smin = smin_t.data() + (size_t)t * nchan;
+        const int64_t trials_run = (count[t] + D - 1) / D * D;  // active waves run all D trials
+        adds_tile += trials_run * ngroups * TT;
+        lds_tile += trials_run * ngroups * TT * 4;  // sum: one window read per trial and group
         tiles[t] = i32x4{first[t], count[t], (int32_t)(TT + spread_t[t] + 1), (int32_t)cb};
         if (dma)
             for (int64_t c = 0; c < nchan; ++c) {
@@ -1338,7 +1344,10 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
                 if (g_end > g && (chans + gs > chan_cap || (used + ns) * 2 * cb > slot_cap)) break;
                 slot_local[g_end] = used;
                 for (const auto &sl : sls) {
-                    slotmeta.push_back((int32_t)(TT + (sl.hi - sl.lo) + 1));
+                    const int64_t len = TT + (sl.hi - sl.lo) + 1;
+                    adds_tile += len * gs;
+                    lds_tile += ((len + 63) / 64 * 64) * (dma ? 4 * G + 8 : 8);  // build reads + 2 writes
+                    slotmeta.push_back((int32_t)len);
                     slotmeta.push_back((int32_t)(used * 2 * cb));
                     slotmeta.push_back((int32_t)c0);
                     slotmeta.push_back(gs);
@@ -1363,6 +1372,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
             }
             stages.push_back(i32x4{g, g_end, s_begin, (int32_t)(slotmeta.size() / ms)});
             tile_stages[t][1]++;
+            if (dma) lds_tile += chans * ((TT + spread_t[t] + 1) * 4 + 255) / 256 * 256;  // DMA writes
             slot_used = std::max(slot_used, used * 2 * cb);
             max_stage_chans = std::max(max_stage_chans, chans);
             g = g_end;
@@ -1410,6 +1420,8 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     p->lds_bytes = (size_t)(raw_used + slot_used);
     p->nslots_total = (int)(slotmeta.size() / ms);
     p->nstages = (int64_t)stages.size();
+    p->exec_adds = adds_tile * ntt;
+    p->lds_traffic = lds_tile * ntt;
     int rc = PU_OK;
     if (!rc) rc = upload(&p->d_tiles, tiles);
     if (!rc) rc = upload(&p->d_tile_stages, tile_stages);
@@ -1551,7 +1563,8 @@ int pu_plan_info(const pu_plan *p, int64_t *info, int n)
     if (!p || !info) return 0;
     const int64_t v[] = {p->ndm, p->ndt, p->ntt, p->group > 1 ? (p->shape == SUB_PAIR ? SubPair::T : SubWide::T) : kTPT, p->TT, p->ncc,
                          p->row_stride, (int64_t)p->lds_bytes, kVariants[p->variant].acc_f64, p->max_spread,
-                         p->group, p->nslots_total, p->nstages, (int64_t)p->slot_bytes, p->raw_stride};
+                         p->group, p->nslots_total, p->nstages, (int64_t)p->slot_bytes, p->raw_stride,
+                         p->exec_adds, p->lds_traffic};
     const int m = std::min<int>(n, (int)(sizeof v / sizeof v[0]));
     for (int k = 0; k < m; ++k) info[k] = v[k];
     return m;

@@ -52,7 +52,7 @@ SIGNATURES = {
 
 INFO_FIELDS = ("ndm", "dm_tiles", "time_tiles", "trials_per_tile", "time_tile", "chans_per_step",
                "row_stride", "lds_bytes", "acc_is_f64", "max_spread", "group", "slots", "stages",
-               "slot_bytes", "raw_stride")
+               "slot_bytes", "raw_stride", "exec_adds", "lds_traffic")
 
 
 class HipBackendError(RuntimeError):
