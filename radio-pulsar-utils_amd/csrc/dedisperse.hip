@@ -196,6 +196,26 @@ __device__ __forceinline__ T wave_sum_to63(T v)
     return v;
 }
 
+// Sum over the wave to lane 63 of per-lane float64 (or float32) partials.  float32
+// partials are summed in float32 within each row of 16 lanes (few terms of one time
+// tile), then in float64 across rows.
+template <typename Ta>
+__device__ __forceinline__ double wave_sum_to63_acc(Ta v)
+{
+    if constexpr (sizeof(Ta) == 8) {
+        return wave_sum_to63(v);
+    } else {
+        v += dpp<0xB1>(Ta(0), v);
+        v += dpp<0x4E>(Ta(0), v);
+        v += dpp<0x124>(Ta(0), v);
+        v += dpp<0x128>(Ta(0), v);
+        double r = static_cast<double>(v);
+        r += dpp<0x142, 0xA>(0.0, r);
+        r += dpp<0x143, 0xC>(0.0, r);
+        return r;
+    }
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_max_to63(T v)
 {
@@ -292,11 +312,17 @@ __device__ __forceinline__ void write_outputs(const Ta (&acc)[D][K], const Dedis
                 }
             }
             double* p = a.partials + ((size_t)(first + slot0 + d) * a.ntt + tt) * kPartStride;
+            const bool full = t0 + J * 64 * E <= n;  // uniform
+            double x1_0 = 0.0;
 #pragma unroll
             for (int w = 0; w < 4; ++w) {
                 const Ta m = wave_max_to63(mx[w]);
-                const double x1 = wave_sum_to63(static_cast<double>(s1[w]));
-                const double x2 = wave_sum_to63(static_cast<double>(s2[w]));
+                // In a full tile every width covers all TT samples, so the shifted sums
+                // of the four rebinned series are the same sum (sum_t x - TT kt): one
+                // reduction serves all widths.
+                const double x1 = (w > 0 && full) ? x1_0 : wave_sum_to63_acc<Ta>(s1[w]);
+                if (w == 0) x1_0 = x1;
+                const double x2 = wave_sum_to63_acc<Ta>(s2[w]);
                 if (lane == 63) {
                     p[1 + 3 * w] = static_cast<double>(m);
                     p[2 + 3 * w] = x1;
