@@ -177,6 +177,33 @@ def test_plane_subband_small_lds_budget(gpu, dt, monkeypatch):
             assert np.all(np.abs(plane[k] - ref) <= f32_bound(x, sh[k])), k
 
 
+@pytest.mark.parametrize("dt", ["u8", "f32"])
+def test_plane_subband_pair_shape(gpu, dt, monkeypatch):
+    """The two-workgroups-per-CU subband shape (PU_SUB_SHAPE=1: 8 waves x 16 trials, time
+    tile 256) against the oracle, ragged N and a partial last group (nchan % 4 != 0)."""
+    c = CONFIGS["C2"]
+    rng = np.random.default_rng(33)
+    nchan, n = 130, 20000 + 37
+    x = rng.random((nchan, n)) * 40
+    x = x.astype(np.uint8) if dt == "u8" else x.astype(np.float32)
+    dms = np.linspace(0.0, 60.0, 150)
+    sh = _hip.shift_table(nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
+    monkeypatch.setenv("PU_SUB_SHAPE", "1")
+    info = {}
+    plane = _plane(x, sh, "native", 4, info)
+    assert info["group"] == 4 and info["time_tile"] == 256, info
+    for k in range(0, 150, 11):
+        ref = oracle.dedisperse(x, sh[k])
+        if dt == "u8":
+            np.testing.assert_array_equal(plane[k].astype(np.float64), ref)
+        else:
+            assert np.all(np.abs(plane[k] - ref) <= f32_bound(x, sh[k])), k
+    g = D._dedispersion_search(x, dms, nchan, c.start_freq, c.bandwidth, c.tsamp)
+    o = oracle.search(x, dms, c.start_freq, c.bandwidth, c.tsamp, nthreads=8)
+    for a, b in zip(g[:3], o[:3]):
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-9)
+
+
 # ------------------------------------------------------------------ search tables
 
 def test_search_test_config_vs_reference(gpu, golden):
