@@ -538,8 +538,8 @@ struct SubArgs {
     DedispArgs o;           // data, ld, nchan, n, ndt, ntt, small_n; plane / partials
     int32_t ngroups;
     int32_t raw_stride;     // floats per staged channel row (DMA mode)
-    int32_t slot_area;      // LDS byte offset of the slot area (after the raw rows)
-    int32_t zero_row;       // LDS byte offset of a zero row (DMA mode), up to slot_area
+    int32_t zero_len;       // floats of the zero row at LDS offset 0 (DMA mode, partial groups)
+    int32_t lds_bytes;      // dynamic LDS size: a stage's raw rows end here
     int32_t skip;           // tuning ablation (PU_SUB_SKIP; results invalid): 1 build, 2 sum, 4 DMA
 };
 
@@ -691,7 +691,7 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
     const bool small_n = o.small_n != 0;
     const Tin *data = reinterpret_cast<const Tin *>(o.data);
     const uint32_t smem_addr = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char *)smem;
-    float *slot_lds = reinterpret_cast<float *>(smem + a.slot_area);
+    float *slot_lds = reinterpret_cast<float *>(smem);  // slot records hold absolute LDS offsets
     const float *raw_lds = reinterpret_cast<const float *>(smem);
 
     float acc[D][K];
@@ -703,8 +703,8 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
     const rec_t *recs = reinterpret_cast<const rec_t *>(rec_tab) + (size_t)dt * a.ngroups * W + wave;
     if constexpr (kDma) {
         // zero row (partial groups' missing channels) between the raw rows and the slots
-        float *zero = reinterpret_cast<float *>(smem + a.zero_row);
-        for (int i = tid; i < (a.slot_area - a.zero_row) / 4; i += C::THREADS) zero[i] = 0.0f;
+        float *zero = reinterpret_cast<float *>(smem);
+        for (int i = tid; i < a.zero_len; i += C::THREADS) zero[i] = 0.0f;
     }
 
     // ---- DMA mode: the channel rows of stage st into the raw area; base0 = this wave's
@@ -713,12 +713,15 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
     auto issue_raw = [&](const i32x4 st, int base0) {
         const int c0 = st.x * G;
         const int nc = min(st.y * G, o.nchan) - c0;
+        // the stage's rows end at the top of LDS (the host packs stages so that they never
+        // overlap the previous stage's slots, which are summed while these rows land)
+        unsigned char *raw = smem + a.lds_bytes - ((nc * a.raw_stride * 4 + 255) & ~255);
         const int cover_bytes = (tile.z * 4 + 255) & ~255;
         for (int ci = wave; ci < nc; ci += W) {
             const int c = c0 + ci;
             int start = (ci == wave ? base0 : ld_uniform(base_t + c)) + t0;
             if (start >= n) start -= n;
-            dma_row_f32(smem + ci * a.raw_stride * 4,
+            dma_row_f32(raw + ci * a.raw_stride * 4,
                         reinterpret_cast<const float *>(data) + (size_t)c * (size_t)o.ld, start, cover_bytes, n,
                         small_n, lane);
         }
@@ -808,7 +811,7 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
             if (k + 1 < ns && !(a.skip & 4)) issue_raw(st1, b1);  // lands while this stage is summed
         }
         if (active && !(a.skip & 2)) {
-            const uint32_t sb = smem_addr + (uint32_t)a.slot_area + 8u * lane;
+            const uint32_t sb = smem_addr + 8u * lane;  // window records: absolute LDS offsets
             rec_t rec = rec0;
             for (int g = st.x; g < st.y; ++g) {
                 const rec_t next = g + 1 < st.y ? ld_uniform(recs + (size_t)(g + 1) * W) : rec;
@@ -934,7 +937,7 @@ struct pu_plan {
     // subband mode (group > 1): per tile {first, count, raw row length, copy bytes},
     // stages {group begin, group end, item begin, item end}, build items, window records
     int group = 1, ngroups = 0, nslots_total = 0, raw_stride = 0, shape = SUB_WIDE;
-    size_t slot_area = 0, slot_bytes = 0, zero_row = 0;
+    size_t slot_bytes = 0, zero_len = 0;
     int64_t exec_adds = 0, lds_traffic = 0;  // per launch (measurement: bench.py roofline)
     int64_t nstages = 0;
     i32x4 *d_tiles = nullptr, *d_stages = nullptr;
@@ -999,8 +1002,8 @@ int launch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
     sa.o = a;
     sa.ngroups = p->ngroups;
     sa.raw_stride = p->raw_stride;
-    sa.slot_area = (int32_t)p->slot_area;
-    sa.zero_row = (int32_t)p->zero_row;
+    sa.zero_len = (int32_t)p->zero_len;
+    sa.lds_bytes = (int32_t)p->lds_bytes;
     if (const char *env = getenv("PU_SUB_SKIP")) sa.skip = atoi(env);
     const dim3 grid((unsigned)((int64_t)p->ndt * p->ntt)), block(C::THREADS);
     if (plane) {
@@ -1224,15 +1227,22 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     const int64_t T = (int64_t)W * D;
     const int ngroups = (int)((nchan + G - 1) / G);
     const bool dma = p->dtype == PU_F32;
-    // raw rows (DMA mode) and slots share the budget; a stage holds whole groups
-    const int64_t raw_cap = dma ? (int64_t)budget * 3 / 10 : 0;
-    const int64_t slot_cap = (int64_t)budget - raw_cap;
+    // a stage's raw rows (DMA mode) and its slots share the LDS budget; a stage holds
+    // whole groups.  The zero row (DMA mode, partial last group) sits at the end.
+    const bool partial = dma && nchan % G != 0;
+    const int64_t lds_cap = (int64_t)budget;
     auto S = [&](int64_t d, int64_t c) { return shifts[d * nchan + c]; };
     auto raw_stride_of = [&](int64_t spread) { return (TT + spread + 1 + 63) / 64 * 64; };
     // slot copy: len = TT + span + 1 elements + 1 padding float (copy 1's element -1)
     auto copy_of = [&](int64_t span) { return (TT + span + 2 + 63) / 64 * 64 * 4; };
-    if (dma && ((G + 1) * raw_stride_of(0) + 64) * 4 > raw_cap) return PU_EUNSUPPORTED;
-    if (2 * copy_of(0) > slot_cap) return PU_EUNSUPPORTED;
+    auto zero_bytes = [&](int64_t stride) { return partial ? ((stride + 64) * 4 + 255) / 256 * 256 : 0; };
+    auto raw_bytes = [&](int64_t chans, int64_t stride) { return dma ? (chans * stride * 4 + 255) / 256 * 256 : 0; };
+    // one group's rows, `slots` slots and the zero row fit the budget
+    auto group_fits = [&](int64_t spread, int64_t slots, int64_t span) {
+        const int64_t rs = raw_stride_of(spread);
+        return raw_bytes(G, rs) + slots * 2 * copy_of(span) + zero_bytes(rs) <= lds_cap;
+    };
+    if (!group_fits(0, 1, 0)) return PU_EUNSUPPORTED;
 
     // ---- relative-shift vector id per (trial, group): v_k = s[c0 + k] - s[c0], k < gs
     std::vector<int32_t> vid((size_t)(ndm * ngroups));
@@ -1283,7 +1293,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
                 for (int64_t c = 0; c < nchan; ++c)
                     sp = std::max(sp, std::max(mx[c], S(j, c)) - std::min(mn[c], S(j, c)));
                 if (sp > kSubMaxSpread) break;
-                if (dma && ((G + 1) * raw_stride_of(sp) + 64) * 4 > raw_cap) break;
+                if (!group_fits(sp, 1, 0)) break;
                 int64_t spn = span;
                 size_t maxslots = 0;
                 for (int g = 0; g < ngroups; ++g) {
@@ -1302,7 +1312,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
                     if (!found) nxt[g].push_back(SubSlot{v, b, b, j});
                     maxslots = std::max(maxslots, nxt[g].size());
                 }
-                if ((int64_t)maxslots * 2 * copy_of(spn) > slot_cap) break;
+                if (!group_fits(sp, (int64_t)maxslots, spn)) break;
                 for (int64_t c = 0; c < nchan; ++c) {
                     mn[c] = std::min(mn[c], S(j, c));
                     mx[c] = std::max(mx[c], S(j, c));
@@ -1327,21 +1337,40 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
         raw_stride = std::max(raw_stride, raw_stride_of(spread_t[t]));
         max_spread = std::max(max_spread, spread_t[t]);
     }
-    // channels one stage may stage (>= G: the widest tile passed G * its stride <= raw_cap)
-    const int64_t chan_cap = dma ? (raw_cap / 4 - raw_stride - 64) / raw_stride : (int64_t)INT32_MAX;
-    if (dma && chan_cap < G) return PU_EUNSUPPORTED;
+    // the plan-wide row stride may exceed a tile's own: every tile's largest group must
+    // still fit with it
+    const int64_t zr = zero_bytes(raw_stride);
+    const int64_t stage_cap = lds_cap - zr;  // raw rows + slots of one stage (and of the
+                                             // next stage's rows + this stage's slots)
+    for (int t = 0; t < ndt; ++t) {
+        size_t maxslots = 0;
+        for (int g = 0; g < ngroups; ++g) maxslots = std::max(maxslots, tslots[(size_t)t * ngroups + g].size());
+        if (raw_bytes(G, raw_stride) + (int64_t)maxslots * 2 * copy_of(span_t[t]) > stage_cap) {
+            pu::set_error("subband mode: a group does not fit the LDS budget");
+            return PU_EUNSUPPORTED;
+        }
+    }
 
-    // ---- stages (consecutive groups whose channels and slots fit), slot records, window
-    // records (D per wave and group), DMA row bases.  DMA mode: a zero row of raw_stride
-    // + 64 floats follows the largest stage's rows (the G - gs missing channels of a
-    // partial group read it, so the build never branches on the group size).
+    // ---- stages, slot records, window records (D per wave and group), DMA row bases.
+    // LDS layout (the budget): [zero row | slots of the stage ... | raw rows of the stage],
+    // the raw rows ending at the top.  Slot and window records hold absolute LDS byte
+    // offsets.  A stage's rows land (DMA) while the previous stage is summed, so they
+    // must also clear the previous stage's slots.  DMA mode: the G - gs missing channels
+    // of a partial last group read the zero row, so the build never branches on the
+    // group size.
     const int ms = slot_stride(G);
-    const int64_t zero_row_f = chan_cap * raw_stride;  // float offset; the raw area is sized below
+    const int64_t zero_row_f = 0;
     std::vector<i32x4> tiles((size_t)ndt), stages;
     std::vector<i32x2> tile_stages((size_t)ndt);
     std::vector<int32_t> slotmeta, base;
     std::vector<uint32_t> rec((size_t)ndt * ngroups * W * D);
-    std::vector<int64_t> slot_local((size_t)ngroups);
+    std::vector<int64_t> slot_local((size_t)ngroups), slot_base((size_t)ngroups);
+    int64_t prev_slots = 0;
+    // float offset of a stage's first raw row: its rows end at the top of LDS
+    auto raw_top_f = [&](int g0, int g1) {
+        const int64_t nc = std::min<int64_t>((int64_t)g1 * G, nchan) - (int64_t)g0 * G;
+        return (lds_cap - raw_bytes(nc, raw_stride)) / 4;
+    };
     int64_t slot_used = 0, max_stage_chans = 0;
     int64_t adds_tile = 0, lds_tile = 0;  // per time tile, summed over DM tiles
     for (int t = 0; t < ndt; ++t) {
@@ -1357,24 +1386,41 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
                 base.push_back((int32_t)(b < 0 ? b + n : b));
             }
         tile_stages[t] = i32x2{(int32_t)stages.size(), 0};
+        prev_slots = 0;
         int g = 0;
         while (g < ngroups) {
             const int32_t s_begin = (int32_t)(slotmeta.size() / ms);
             int64_t used = 0, chans = 0;
+            int g_stop = g;  // pass 1: the stage's group range
+            {
+                int64_t u = 0, ch = 0;
+                while (g_stop < ngroups) {
+                    const int gs = (int)std::min<int64_t>(G, nchan - (int64_t)g_stop * G);
+                    const int64_t ns = (int64_t)tslots[(size_t)t * ngroups + g_stop].size();
+                    const int64_t rb = raw_bytes(ch + gs, raw_stride);
+                    if (g_stop > g && (rb + (u + ns) * 2 * cb > stage_cap || rb + prev_slots > stage_cap)) break;
+                    u += ns;
+                    ch += gs;
+                    ++g_stop;
+                }
+                if (raw_bytes(ch, raw_stride) + prev_slots > stage_cap) {
+                    pu::set_error("subband mode: consecutive stages do not fit the LDS budget");
+                    return PU_EUNSUPPORTED;
+                }
+                prev_slots = u * 2 * cb;
+            }
             int g_end = g;
-            while (g_end < ngroups) {
+            while (g_end < g_stop) {
                 const int64_t c0 = (int64_t)g_end * G;
                 const int gs = (int)std::min<int64_t>(G, nchan - c0);
                 const auto &sls = tslots[(size_t)t * ngroups + g_end];
-                const int64_t ns = (int64_t)sls.size();
-                if (g_end > g && (chans + gs > chan_cap || (used + ns) * 2 * cb > slot_cap)) break;
                 slot_local[g_end] = used;
                 for (const auto &sl : sls) {
                     const int64_t len = TT + (sl.hi - sl.lo) + 1;
                     adds_tile += len * gs;
                     lds_tile += ((len + 63) / 64 * 64) * (dma ? 4 * G + 8 : 8);  // build reads + 2 writes
                     slotmeta.push_back((int32_t)len);
-                    slotmeta.push_back((int32_t)(used * 2 * cb));
+                    slotmeta.push_back((int32_t)(zr + used * 2 * cb));
                     slotmeta.push_back((int32_t)c0);
                     slotmeta.push_back(gs);
                     for (int k = 0; k < ms - 4; ++k) {
@@ -1383,7 +1429,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
                             // smallest shift of channel c0+k over the slot's trials
                             const int64_t sk = sl.lo + S(sl.d0, c0 + k) - S(sl.d0, c0);
                             if (dma) {
-                                src = (chans + k) * raw_stride + (sk - smin[c0 + k]);
+                                src = raw_top_f(g, g_stop) + (chans + k) * raw_stride + (sk - smin[c0 + k]);
                             } else {
                                 src = sk % n;
                                 if (src < 0) src += n;
@@ -1399,7 +1445,8 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
             stages.push_back(i32x4{g, g_end, s_begin, (int32_t)(slotmeta.size() / ms)});
             tile_stages[t][1]++;
             if (dma) lds_tile += chans * ((TT + spread_t[t] + 1) * 4 + 255) / 256 * 256;  // DMA writes
-            slot_used = std::max(slot_used, used * 2 * cb);
+            slot_used = std::max(slot_used, zr + used * 2 * cb);
+            for (int gg = g; gg < g_end; ++gg) slot_base[gg] = zr;
             max_stage_chans = std::max(max_stage_chans, chans);
             g = g_end;
         }
@@ -1413,14 +1460,15 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
                     size_t si = 0;
                     while (sls[si].vid != v) ++si;
                     const int64_t rr = S(tr, (int64_t)gg * G) - sls[si].lo;
-                    r[d] = (uint32_t)((slot_local[gg] + (int64_t)si) * 2 * cb + (rr & 1) * cb + (rr & ~int64_t(1)) * 4);
+                    r[d] = (uint32_t)(slot_base[gg] + (slot_local[gg] + (int64_t)si) * 2 * cb + (rr & 1) * cb +
+                                      (rr & ~int64_t(1)) * 4);
                 }
             }
         }
     }
-    const int64_t raw_used = dma ? ((chan_cap * raw_stride + raw_stride + 64) * 4 + 255) / 256 * 256 : 0;
-    if (raw_used + slot_used > 160 * 1024) {
-        pu::set_error("subband mode: %lld bytes of LDS", (long long)(raw_used + slot_used));
+    const int64_t lds_total = lds_cap;
+    if (lds_total > 160 * 1024) {
+        pu::set_error("subband mode: %lld bytes of LDS", (long long)lds_total);
         return PU_EUNSUPPORTED;
     }
     const int64_t ntt = (n + TT - 1) / TT;
@@ -1440,10 +1488,9 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     p->row_stride = (int)raw_stride;
     p->max_spread = (int)max_spread;
     p->small_n = raw_stride + 2 > n ? 1 : 0;
-    p->slot_area = (size_t)raw_used;
-    p->zero_row = dma ? (size_t)(zero_row_f * 4) : (size_t)raw_used;
+    p->zero_len = zr ? (size_t)(raw_stride + 64) : 0;
     p->slot_bytes = (size_t)slot_used;
-    p->lds_bytes = (size_t)(raw_used + slot_used);
+    p->lds_bytes = (size_t)lds_total;
     p->nslots_total = (int)(slotmeta.size() / ms);
     p->nstages = (int64_t)stages.size();
     p->exec_adds = adds_tile * ntt;
