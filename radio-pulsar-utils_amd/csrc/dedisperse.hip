@@ -669,7 +669,8 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
     constexpr bool kDma = std::is_same<Tin, float>::value;
     constexpr int W = C::W, D = C::D, K = C::K, TT = C::TT;
     constexpr int MS = slot_stride(G);
-    constexpr int U = ((TT + 80 + 63) / 64 + 1) / 2;  // chunks per build pass (two at a plan grid's spread)
+    // chunks of 64 per build pass: one pass at a plan grid's spread when G x U values fit
+    constexpr int U = std::min((TT + 80 + 63) / 64, (sizeof(Tin) == 8 ? 20 : 40) / G);
     typedef int32_t meta_t __attribute__((ext_vector_type(MS)));
     typedef uint32_t rec_t __attribute__((ext_vector_type(D)));
     const DedispArgs &o = a.o;
