@@ -14,17 +14,24 @@
 // the rounding of x*f - mu and of the squared deviations.
 //
 // Kernels
-//   rowsum_chunk_kernel  one workgroup per (row, full 8192 block): LDS-staged leaves,
-//                        8-accumulator leaf sums, in-order pairwise tree.
+//   rowsum_chunk_kernel  one workgroup per (row, full 8192 block): leaves read straight
+//                        into registers, 8-accumulator leaf sums, in-order pairwise
+//                        tree by xor-shuffles.
 //   rowsum_tail_kernel   one lane per row for the trailing partial block (irregular
 //                        pairwise tree; compile-time-bounded recursion).
 //   rowsum_combine       sequential 0 + block sums (+ true_divide by the count).
-//   colmean_kernel       one lane per column, rows in order (clean.py:77).
-//   gauss_kernel         scipy correlate1d symmetric order, mode 'reflect' (:79).
-//   apply_kernel         (x*f - mu)/mu, bad rows zeroed, optional column mean (:81-94).
+//   colmean_kernel       V adjacent columns per lane, rows in order (clean.py:77).
+//   gauss_lds_kernel     scipy correlate1d symmetric order, mode 'reflect' (:79), from
+//                        an LDS window (gauss_kernel: direct form for huge radii).
+//   apply_kernel         (x*f - mu)/mu, bad rows zeroed, optional column mean (:81-94),
+//                        V adjacent columns per lane.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <type_traits>
 
 #include "pu_common.h"
 
@@ -32,7 +39,7 @@ namespace {
 
 constexpr int kBlock = 8192;   // numpy ufunc buffer size
 constexpr int kLeaf = 128;     // numpy PW_BLOCKSIZE
-constexpr int kLeafPad = 8;    // LDS padding per leaf (bank spread)
+constexpr int kScaleRows = 4;  // rows per workgroup of the scaled (MODE 2) row sums
 
 template <typename Tin, typename Ta, int MODE>
 __device__ __forceinline__ Ta load_val(const Tin *row, int64_t t, Ta center, const double *scale)
@@ -81,45 +88,105 @@ __device__ Ta pairwise_lane(const Tin *row, int64_t off, int64_t n, Ta center, c
     return res;
 }
 
-// Full 8192-element blocks: 64 leaves of 128.  Thread (b = tid/4, q = tid%4) owns
-// accumulators r[2q], r[2q+1] of leaf b; the leaf total is
-// ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) via two xor-shuffles, then the 64 leaves
-// combine as the perfect binary tree pairwise_sum builds for n = 8192.
+// V consecutive elements moved by one global load / store instruction.
+template <typename T, int V>
+struct alignas(sizeof(T) * V) Vec {
+    T v[V];
+};
+
+template <typename T, int V>
+__device__ __forceinline__ Vec<T, V> load_vec(const T *p)
+{
+    return *reinterpret_cast<const Vec<T, V> *>(p);
+}
+
+// load_val on an element already in registers (s = scale[t] for MODE 2).
 template <typename Tin, typename Ta, int MODE>
+__device__ __forceinline__ Ta elem_val(Tin x, Ta center, double s)
+{
+    if constexpr (MODE == 0) {
+        return static_cast<Ta>(x);
+    } else if constexpr (MODE == 1) {
+        const Ta d = static_cast<Ta>(x) - center;
+        return d * d;
+    } else if constexpr (MODE == 4) {
+        const Ta v = static_cast<Ta>(x);
+        return v * v;
+    } else {
+        return static_cast<Ta>(static_cast<double>(x) * s);
+    }
+}
+
+// Full 8192-element blocks: 64 leaves of 128, read straight into registers.
+// Thread (b = tid/4, q = tid%4) owns accumulators r[2q], r[2q+1] of leaf b and loads
+// its 16 element pairs (stride 8) with all loads in flight; the leaf total is
+// ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) via two xor-shuffles.  The 64 leaves combine
+// as the perfect binary tree pairwise_sum builds for n = 8192: leaf distances 1..8
+// are lane distances 4..32 inside a wave (left + right at the even lane), the last
+// two levels are (W0+W1)+(W2+W3) over the four waves.  PAIR: element pairs (and
+// the scale pairs of MODE 2) are single 2-element vector loads.  A workgroup sums
+// the same block of R consecutive rows, so MODE 2 reads its scale pairs once per R
+// rows instead of once per row.
+template <typename Tin, typename Ta, int MODE, bool PAIR, int R>
 __global__ void __launch_bounds__(256)
-rowsum_chunk_kernel(const Tin *__restrict__ x, int64_t ld, int64_t nfull, int64_t nblk_row,
+rowsum_chunk_kernel(const Tin *__restrict__ x, int64_t ld, int64_t nrows, int64_t nfull, int64_t nblk_row,
                     const Ta *__restrict__ centers, const double *__restrict__ scale,
                     Ta *__restrict__ block_sums)
 {
-    __shared__ Ta buf[64 * (kLeaf + kLeafPad)];
-    __shared__ Ta leaves[64];
-    const int64_t row = blockIdx.x / nfull;
+    __shared__ Ta wave_tot[R][4];
+    const int64_t row0 = (blockIdx.x / nfull) * R;
     const int64_t blk = blockIdx.x % nfull;
     const int tid = threadIdx.x;
-    const Tin *rp = x + row * ld;
-    const Ta center = MODE == 1 ? centers[row] : Ta(0);
-    const int64_t off = blk * kBlock;
-    for (int e = tid; e < kBlock; e += 256)
-        buf[(e >> 7) * (kLeaf + kLeafPad) + (e & 127)] = load_val<Tin, Ta, MODE>(rp, off + e, center, scale);
-    __syncthreads();
     const int b = tid >> 2, q = tid & 3;
-    const Ta *lp = buf + b * (kLeaf + kLeafPad) + 2 * q;
-    Ta r0 = lp[0], r1 = lp[1];
+    const int64_t e0 = blk * kBlock + b * kLeaf + 2 * q;
+    double sa[16], sc[16];
 #pragma unroll
-    for (int m = 1; m < 16; ++m) {
-        r0 += lp[8 * m];
-        r1 += lp[8 * m + 1];
+    for (int m = 0; m < 16; ++m) {
+        if constexpr (MODE == 2 && PAIR) {
+            const Vec<double, 2> s = load_vec<double, 2>(scale + e0 + 8 * m);
+            sa[m] = s.v[0];
+            sc[m] = s.v[1];
+        } else if constexpr (MODE == 2) {
+            sa[m] = scale[e0 + 8 * m];
+            sc[m] = scale[e0 + 8 * m + 1];
+        } else {
+            sa[m] = sc[m] = 0.0;
+        }
     }
-    Ta t = r0 + r1;
-    t += __shfl_xor(t, 1, 64);
-    t += __shfl_xor(t, 2, 64);
-    if (q == 0) leaves[b] = t;
+#pragma unroll
+    for (int rr = 0; rr < R; ++rr) {
+        const int64_t row = row0 + rr;
+        if (row >= nrows) break;
+        const Tin *rp = x + row * ld + e0;
+        const Ta center = MODE == 1 ? centers[row] : Ta(0);
+        Tin a[16], c[16];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            if constexpr (PAIR) {
+                const Vec<Tin, 2> p = load_vec<Tin, 2>(rp + 8 * m);
+                a[m] = p.v[0];
+                c[m] = p.v[1];
+            } else {
+                a[m] = rp[8 * m];
+                c[m] = rp[8 * m + 1];
+            }
+        }
+        Ta r0 = elem_val<Tin, Ta, MODE>(a[0], center, sa[0]);
+        Ta r1 = elem_val<Tin, Ta, MODE>(c[0], center, sc[0]);
+#pragma unroll
+        for (int m = 1; m < 16; ++m) {
+            r0 += elem_val<Tin, Ta, MODE>(a[m], center, sa[m]);
+            r1 += elem_val<Tin, Ta, MODE>(c[m], center, sc[m]);
+        }
+        Ta t = r0 + r1;
+#pragma unroll
+        for (int s = 1; s < 64; s <<= 1) t += __shfl_xor(t, s, 64);
+        if ((tid & 63) == 0) wave_tot[rr][tid >> 6] = t;
+    }
     __syncthreads();
-    for (int s = 1; s < 64; s <<= 1) {
-        if (tid < 64 && (tid % (2 * s)) == 0) leaves[tid] = leaves[tid] + leaves[tid + s];
-        __syncthreads();
-    }
-    if (tid == 0) block_sums[row * nblk_row + blk] = leaves[0];
+    if (tid < R && row0 + tid < nrows)
+        block_sums[(row0 + tid) * nblk_row + blk] =
+            (wave_tot[tid][0] + wave_tot[tid][1]) + (wave_tot[tid][2] + wave_tot[tid][3]);
 }
 
 template <typename Tin, typename Ta, int MODE>
@@ -148,20 +215,81 @@ __global__ void rowsum_combine(const Ta *__restrict__ block_sums, int64_t nrows,
     out[row] = acc;
 }
 
-template <typename Tin>
-__global__ void colmean_kernel(const Tin *__restrict__ x, int64_t nrows, int64_t n, int64_t ld,
-                               const uint8_t *__restrict__ skip, double *__restrict__ out)
+// Column passes: a lane owns V adjacent columns and walks the rows in order (the
+// numpy order of mean(0) and of the row loop of clean.py:81-94).  Per-row scalars
+// (skip flag, channel mean) are staged in LDS per chunk of kRowChunk rows.
+constexpr int kRowChunk = 4096;
+constexpr int kBatchBytes = 128;  // per lane and register buffer: U = kBatchBytes / (V * elem)
+constexpr int kMaxBatchRows = 32;
+
+// Rows [0, rn) of a column strip, in order: batches of U rows alternate between two
+// register buffers, the next batch's loads issued before the current batch is
+// consumed (no register copies, so a wait never covers the batch in flight).
+template <typename Tin, int V, typename Body>
+__device__ __forceinline__ void walk_rows(const Tin *p, int64_t ld, int rn, Body &&body)
 {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
-    double acc = 0.0;
-    int64_t ngood = 0;
-    for (int64_t r = 0; r < nrows; ++r) {
-        if (skip && skip[r]) continue;
-        acc += static_cast<double>(x[r * ld + t]);
-        ++ngood;
+    constexpr int U = std::max(1, std::min(kMaxBatchRows, kBatchBytes / (V * (int)sizeof(Tin))));
+    Vec<Tin, V> a[U], b[U];
+    auto load = [&](Vec<Tin, V>(&dst)[U], int i0) {
+        if (i0 + U <= rn) {
+#pragma unroll
+            for (int k = 0; k < U; ++k) dst[k] = load_vec<Tin, V>(p + (int64_t)(i0 + k) * ld);
+        } else {
+#pragma unroll
+            for (int k = 0; k < U; ++k)
+                if (i0 + k < rn) dst[k] = load_vec<Tin, V>(p + (int64_t)(i0 + k) * ld);
+        }
+    };
+    auto run = [&](Vec<Tin, V>(&src)[U], int i0) {
+        if (i0 + U <= rn) {
+#pragma unroll
+            for (int k = 0; k < U; ++k) body(i0 + k, src[k]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < U; ++k)
+                if (i0 + k < rn) body(i0 + k, src[k]);
+        }
+    };
+    load(a, 0);
+    for (int i0 = 0; i0 < rn; i0 += 2 * U) {
+        if (i0 + U < rn) load(b, i0 + U);
+        run(a, i0);
+        if (i0 + 2 * U < rn) load(a, i0 + 2 * U);
+        if (i0 + U < rn) run(b, i0 + U);
     }
-    out[t] = acc / static_cast<double>(ngood);
+}
+
+// Skipped rows add +0.0 (a select, not a branch): acc starts at +0.0 and never
+// becomes -0.0 under round-to-nearest, so acc + 0.0 == acc bit for bit, and NaN or
+// Inf in a skipped row never reaches the sum.
+template <typename Tin, int V>
+__global__ void __launch_bounds__(256)
+colmean_kernel(const Tin *__restrict__ x, int64_t nrows, int64_t col0, int64_t ncols, int64_t ld,
+               const uint8_t *__restrict__ skip, double *__restrict__ out)
+{
+    __shared__ uint8_t sk[kRowChunk];
+    const int64_t c = col0 + ((int64_t)blockIdx.x * 256 + threadIdx.x) * V;
+    const bool active = c < col0 + ncols;
+    double acc[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) acc[j] = 0.0;
+    int64_t ngood = 0;
+    for (int64_t r0 = 0; r0 < nrows; r0 += kRowChunk) {
+        const int rn = (int)(nrows - r0 < kRowChunk ? nrows - r0 : kRowChunk);
+        __syncthreads();
+        for (int i = threadIdx.x; i < rn; i += 256) sk[i] = skip ? skip[r0 + i] : 0;
+        __syncthreads();
+        for (int i = 0; i < rn; ++i) ngood += sk[i] ? 0 : 1;
+        if (!active) continue;
+        walk_rows<Tin, V>(x + r0 * ld + c, ld, rn, [&](int i, const Vec<Tin, V> &v) {
+            const bool s = sk[i] != 0;
+#pragma unroll
+            for (int j = 0; j < V; ++j) acc[j] += s ? 0.0 : static_cast<double>(v.v[j]);
+        });
+    }
+    if (!active) return;
+#pragma unroll
+    for (int j = 0; j < V; ++j) out[c + j] = acc[j] / static_cast<double>(ngood);
 }
 
 __device__ __forceinline__ int64_t reflect_index(int64_t i, int64_t n)
@@ -173,6 +301,7 @@ __device__ __forceinline__ int64_t reflect_index(int64_t i, int64_t n)
     return m >= n ? p - 1 - m : m;
 }
 
+// Direct form (radius too large for the LDS window).
 __global__ void gauss_kernel(const double *__restrict__ x, int64_t n, const double *__restrict__ w,
                              int64_t r, double *__restrict__ out)
 {
@@ -184,31 +313,91 @@ __global__ void gauss_kernel(const double *__restrict__ x, int64_t n, const doub
     out[i] = acc;
 }
 
+// LDS form: a workgroup stages its 256 outputs' window x[i0-r, i0+256+r) (reflected
+// once, at staging) and the r+1 weights, then every tap is two LDS reads and one
+// broadcast read, in scipy's symmetric order.
+constexpr int kGaussMaxR = 2048;
+
+__global__ void __launch_bounds__(256)
+gauss_lds_kernel(const double *__restrict__ x, int64_t n, const double *__restrict__ w, int r,
+                 double *__restrict__ out)
+{
+    extern __shared__ double gsm[];
+    double *ws = gsm;              // r + 1 weights
+    double *xs = gsm + (r + 1);    // 256 + 2r window
+    const int64_t i0 = (int64_t)blockIdx.x * 256;
+    for (int k = threadIdx.x; k <= r; k += 256) ws[k] = w[k];
+    for (int k = threadIdx.x; k < 256 + 2 * r; k += 256) {
+        const int64_t g = i0 - r + k;
+        xs[k] = x[(g >= 0 && g < n) ? g : reflect_index(g, n)];
+    }
+    __syncthreads();
+    const int64_t i = i0 + threadIdx.x;
+    if (i >= n) return;
+    const double *xc = xs + r + threadIdx.x;
+    double acc = xc[0] * ws[r];
+    for (int jj = -r; jj < 0; ++jj) acc += (xc[jj] + xc[-jj]) * ws[r + jj];
+    out[i] = acc;
+}
+
 __global__ void ratio_kernel(double num, const double *__restrict__ x, int64_t n, double *__restrict__ out)
 {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = num / x[i];
 }
 
-template <typename Tin>
-__global__ void apply_kernel(const Tin *__restrict__ x, int64_t nchan, int64_t n, int64_t ld,
-                             const double *__restrict__ factor, const double *__restrict__ spec,
-                             const uint8_t *__restrict__ bad, double *__restrict__ out, int64_t ld_out,
-                             double *__restrict__ col_means)
+// (x*f - mu)/mu per element, bad channels written as 0.0, column mean of the result
+// accumulated over channels in order.  Same column layout as colmean_kernel; the
+// channel means and bad flags are staged in LDS per row chunk.
+template <typename Tin, int V, bool NT>
+__global__ void __launch_bounds__(256)
+apply_kernel(const Tin *__restrict__ x, int64_t nchan, int64_t col0, int64_t ncols, int64_t ld,
+             const double *__restrict__ factor, const double *__restrict__ spec,
+             const uint8_t *__restrict__ bad, double *__restrict__ out, int64_t ld_out,
+             double *__restrict__ col_means)
 {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
-    const double f = factor[t];
-    double acc = 0.0;
-    for (int64_t c = 0; c < nchan; ++c) {
-        double v = static_cast<double>(x[c * ld + t]) * f;
-        const double mu = spec[c];
-        v = (v - mu) / mu;
-        if (bad && bad[c]) v = 0.0;
-        out[c * ld_out + t] = v;
-        acc += v;
+    __shared__ double mus[kRowChunk];
+    __shared__ uint8_t bads[kRowChunk];
+    const int64_t c = col0 + ((int64_t)blockIdx.x * 256 + threadIdx.x) * V;
+    const bool active = c < col0 + ncols;
+    double f[V], acc[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+        f[j] = active ? factor[c + j] : 0.0;
+        acc[j] = 0.0;
     }
-    if (col_means) col_means[t] = acc / static_cast<double>(nchan);
+    for (int64_t r0 = 0; r0 < nchan; r0 += kRowChunk) {
+        const int rn = (int)(nchan - r0 < kRowChunk ? nchan - r0 : kRowChunk);
+        __syncthreads();
+        for (int i = threadIdx.x; i < rn; i += 256) {
+            mus[i] = spec[r0 + i];
+            bads[i] = bad ? bad[r0 + i] : 0;
+        }
+        __syncthreads();
+        if (!active) continue;
+        double *o = out + r0 * ld_out + c;
+        walk_rows<Tin, V>(x + r0 * ld + c, ld, rn, [&](int i, const Vec<Tin, V> &v) {
+            const double mu = mus[i];
+            const bool b = bads[i] != 0;
+            Vec<double, V> res;
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                double e = static_cast<double>(v.v[j]) * f[j];
+                e = (e - mu) / mu;
+                res.v[j] = b ? 0.0 : e;
+                acc[j] += res.v[j];
+            }
+            if constexpr (NT) {
+#pragma unroll
+                for (int j = 0; j < V; ++j) __builtin_nontemporal_store(res.v[j], o + (int64_t)i * ld_out + j);
+            } else {
+                *reinterpret_cast<Vec<double, V> *>(o + (int64_t)i * ld_out) = res;
+            }
+        });
+    }
+    if (!active || !col_means) return;
+#pragma unroll
+    for (int j = 0; j < V; ++j) col_means[c + j] = acc[j] / static_cast<double>(nchan);
 }
 
 __global__ void zero_cols_kernel(double *out, int64_t nrows, int64_t ld, const int64_t *__restrict__ cols,
@@ -231,9 +420,18 @@ int row_sums_t(const void *x, int64_t nrows, int64_t n, int64_t ld, const void *
     const Tin *xp = reinterpret_cast<const Tin *>(x);
     const Ta *cp = reinterpret_cast<const Ta *>(center);
     if (nfull > 0) {
-        PU_REQUIRE(nrows * nfull < (int64_t(1) << 31), "pu_row_sums: too many blocks");
-        hipLaunchKernelGGL((rowsum_chunk_kernel<Tin, Ta, MODE>), dim3((unsigned)(nrows * nfull)), dim3(256), 0, s,
-                           xp, ld, nfull, nblk_row, cp, scale, bs);
+        // pair loads need 2-element alignment of every row (and of the scale vector)
+        const bool pair = reinterpret_cast<uintptr_t>(x) % (2 * sizeof(Tin)) == 0 && ld % 2 == 0 &&
+                          (MODE != 2 || reinterpret_cast<uintptr_t>(scale) % 16 == 0);
+        constexpr int R = MODE == 2 ? kScaleRows : 1;
+        const int64_t ngroups = (nrows + R - 1) / R;
+        PU_REQUIRE(ngroups * nfull < (int64_t(1) << 31), "pu_row_sums: too many blocks");
+        if (pair)
+            hipLaunchKernelGGL((rowsum_chunk_kernel<Tin, Ta, MODE, true, R>), dim3((unsigned)(ngroups * nfull)),
+                               dim3(256), 0, s, xp, ld, nrows, nfull, nblk_row, cp, scale, bs);
+        else
+            hipLaunchKernelGGL((rowsum_chunk_kernel<Tin, Ta, MODE, false, R>), dim3((unsigned)(ngroups * nfull)),
+                               dim3(256), 0, s, xp, ld, nrows, nfull, nblk_row, cp, scale, bs);
         int rc = pu::launch_check("rowsum_chunk_kernel");
         if (rc) return rc;
     }
@@ -264,6 +462,87 @@ int row_sums_in(int mode, bool f32acc, const void *x, int64_t nrows, int64_t n, 
 }
 
 unsigned blocks_for(int64_t n, int threads) { return (unsigned)((n + threads - 1) / threads); }
+
+// Widest V in {vmax, .., 2} with every row start of p (stride ld elements) aligned
+// to V elements; 1 otherwise.
+template <typename T>
+int pick_vec(const void *p, int64_t ld, int vmax)
+{
+    for (int v = vmax; v > 1; v >>= 1)
+        if (reinterpret_cast<uintptr_t>(p) % (v * sizeof(T)) == 0 && ld % v == 0) return v;
+    return 1;
+}
+
+// Column lanes: V adjacent columns per lane (16-byte loads at most).  Measured on C4
+// (1024 x 2^18): the read-only mean pass is fastest with wide lanes (V=4), the
+// apply pass (float64 stores, a division per element) with the most waves (V=1).
+// PU_CLEAN_VMAX overrides both (1, 2 or 4).
+int vec_max(size_t elem, int dflt)
+{
+    static const int env = [] {
+        const char *e = getenv("PU_CLEAN_VMAX");
+        return e ? atoi(e) : 0;
+    }();
+    const int v = env > 0 ? env : dflt;
+    const int w = v >= 4 ? 4 : v >= 2 ? 2 : 1;
+    return elem >= 8 && w > 2 ? 2 : w;
+}
+
+// Columns [0, n - n%V) with V-wide lanes, the rest with scalar lanes.
+template <typename Tin, typename Launch>
+int column_launches(int v, int64_t n, Launch &&launch)
+{
+    const int64_t nv = n - n % v;
+    if (nv > 0) {
+        if constexpr (sizeof(Tin) < 8)
+            if (v == 4) launch(std::integral_constant<int, 4>{}, 0, nv);
+        if (v == 2) launch(std::integral_constant<int, 2>{}, 0, nv);
+        if (v == 1) launch(std::integral_constant<int, 1>{}, 0, nv);
+    }
+    if (n > nv) launch(std::integral_constant<int, 1>{}, nv, n - nv);
+    return PU_OK;
+}
+
+template <typename Tin>
+int col_means_t(const void *x, int64_t nrows, int64_t n, int64_t ld, const uint8_t *skip, double *out, hipStream_t s)
+{
+    const int v = pick_vec<Tin>(x, ld, vec_max(sizeof(Tin), 4));
+    return column_launches<Tin>(v, n, [&](auto vc, int64_t col0, int64_t ncols) {
+        constexpr int V = decltype(vc)::value;
+        hipLaunchKernelGGL((colmean_kernel<Tin, V>), dim3(blocks_for(ncols / V, 256)), dim3(256), 0, s,
+                           reinterpret_cast<const Tin *>(x), nrows, col0, ncols, ld, skip, out);
+    });
+}
+
+// Output plane written with non-temporal stores: on for 8-bit input (C4 u8 apply
+// 542 -> 481 us), off for float input (606 vs 623 us); PU_CLEAN_NT=0/1 overrides.
+bool nt_stores(size_t elem)
+{
+    static const int env = [] {
+        const char *e = getenv("PU_CLEAN_NT");
+        return e ? atoi(e) : -1;
+    }();
+    return env >= 0 ? env != 0 : elem == 1;
+}
+
+template <typename Tin>
+int renorm_apply_t(const void *x, int64_t nchan, int64_t n, int64_t ld, const double *factor, const double *spec,
+                   const uint8_t *bad, double *out, int64_t ld_out, double *col_means, hipStream_t s)
+{
+    const int vm = vec_max(sizeof(Tin), 1);
+    const int v = std::min(pick_vec<Tin>(x, ld, vm), pick_vec<double>(out, ld_out, vm));
+    return column_launches<Tin>(v, n, [&](auto vc, int64_t col0, int64_t ncols) {
+        constexpr int V = decltype(vc)::value;
+        if (nt_stores(sizeof(Tin)))
+            hipLaunchKernelGGL((apply_kernel<Tin, V, true>), dim3(blocks_for(ncols / V, 256)), dim3(256), 0, s,
+                               reinterpret_cast<const Tin *>(x), nchan, col0, ncols, ld, factor, spec, bad, out,
+                               ld_out, col_means);
+        else
+            hipLaunchKernelGGL((apply_kernel<Tin, V, false>), dim3(blocks_for(ncols / V, 256)), dim3(256), 0, s,
+                               reinterpret_cast<const Tin *>(x), nchan, col0, ncols, ld, factor, spec, bad, out,
+                               ld_out, col_means);
+    });
+}
 
 }  // namespace
 
@@ -300,17 +579,10 @@ int pu_col_means(const void *x, int dtype, int64_t nrows, int64_t n, int64_t ld,
     PU_REQUIRE(x && out, "pu_col_means: NULL pointer");
     PU_REQUIRE(nrows > 0 && n > 0 && ld >= n, "pu_col_means: bad shape");
     hipStream_t s = pu::as_stream(stream);
-    const dim3 g(blocks_for(n, 256)), b(256);
     switch (dtype) {
-    case PU_U8:
-        hipLaunchKernelGGL(colmean_kernel<uint8_t>, g, b, 0, s, (const uint8_t *)x, nrows, n, ld, skip, out);
-        break;
-    case PU_F32:
-        hipLaunchKernelGGL(colmean_kernel<float>, g, b, 0, s, (const float *)x, nrows, n, ld, skip, out);
-        break;
-    case PU_F64:
-        hipLaunchKernelGGL(colmean_kernel<double>, g, b, 0, s, (const double *)x, nrows, n, ld, skip, out);
-        break;
+    case PU_U8: col_means_t<uint8_t>(x, nrows, n, ld, skip, out, s); break;
+    case PU_F32: col_means_t<float>(x, nrows, n, ld, skip, out, s); break;
+    case PU_F64: col_means_t<double>(x, nrows, n, ld, skip, out, s); break;
     default: pu::set_error("pu_col_means: unsupported dtype %d", dtype); return PU_EUNSUPPORTED;
     }
     return pu::launch_check("colmean_kernel");
@@ -319,6 +591,12 @@ int pu_col_means(const void *x, int dtype, int64_t nrows, int64_t n, int64_t ld,
 int pu_gaussian_filter1d(const double *x, int64_t n, const double *w, int64_t r, double *out, void *stream)
 {
     PU_REQUIRE(x && w && out && n > 0 && r >= 0, "pu_gaussian_filter1d: bad arguments");
+    if (r <= kGaussMaxR) {
+        const size_t lds = (size_t)(r + 1 + 256 + 2 * r) * sizeof(double);
+        hipLaunchKernelGGL(gauss_lds_kernel, dim3(blocks_for(n, 256)), dim3(256), lds, pu::as_stream(stream), x, n, w,
+                           (int)r, out);
+        return pu::launch_check("gauss_lds_kernel");
+    }
     hipLaunchKernelGGL(gauss_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, pu::as_stream(stream), x, n, w, r, out);
     return pu::launch_check("gauss_kernel");
 }
@@ -337,20 +615,10 @@ int pu_renorm_apply(const void *x, int dtype, int64_t nchan, int64_t n, int64_t 
     PU_REQUIRE(x && factor && spec && out, "pu_renorm_apply: NULL pointer");
     PU_REQUIRE(nchan > 0 && n > 0 && ld >= n && ld_out >= n, "pu_renorm_apply: bad shape");
     hipStream_t s = pu::as_stream(stream);
-    const dim3 g(blocks_for(n, 256)), b(256);
     switch (dtype) {
-    case PU_U8:
-        hipLaunchKernelGGL(apply_kernel<uint8_t>, g, b, 0, s, (const uint8_t *)x, nchan, n, ld, factor, spec, bad,
-                           out, ld_out, col_means);
-        break;
-    case PU_F32:
-        hipLaunchKernelGGL(apply_kernel<float>, g, b, 0, s, (const float *)x, nchan, n, ld, factor, spec, bad, out,
-                           ld_out, col_means);
-        break;
-    case PU_F64:
-        hipLaunchKernelGGL(apply_kernel<double>, g, b, 0, s, (const double *)x, nchan, n, ld, factor, spec, bad,
-                           out, ld_out, col_means);
-        break;
+    case PU_U8: renorm_apply_t<uint8_t>(x, nchan, n, ld, factor, spec, bad, out, ld_out, col_means, s); break;
+    case PU_F32: renorm_apply_t<float>(x, nchan, n, ld, factor, spec, bad, out, ld_out, col_means, s); break;
+    case PU_F64: renorm_apply_t<double>(x, nchan, n, ld, factor, spec, bad, out, ld_out, col_means, s); break;
     default: pu::set_error("pu_renorm_apply: unsupported dtype %d", dtype); return PU_EUNSUPPORTED;
     }
     return pu::launch_check("apply_kernel");

@@ -78,3 +78,26 @@ def test_renormalize_api_matches_oracle_small(gpu):
     np.testing.assert_array_equal(C.renormalize_data(x, badchans_mask=bad, cut_outliers=True),
                                   co.renormalize(x, badchans_mask=bad, cut_outliers=True))
     np.testing.assert_array_equal(C.renormalize_data(x), co.renormalize(x))
+
+
+@pytest.mark.parametrize("dt", ["f32", "u8", "f64"])
+@pytest.mark.parametrize("n,pad,off", [(12346, 6, 0), (16388, 4, 2), (8192 * 2 + 8, 0, 1)])
+def test_clean_strided_views(gpu, dt, n, pad, off):
+    """Row stride / base alignment select the vector width of the column and row
+    kernels (4, 2 or 1 elements): padded and offset views match numpy bit for bit."""
+    import torch
+    from pulsarutils import _hip
+    rag = replace(CONFIGS["C4"], nchan=37, nsamples=n, seed=5)
+    x = synth.rfi_filterbank_np(rag, dtype=dt)
+    big = np.zeros((x.shape[0], off + n + pad), dtype=x.dtype)
+    big[:, off:off + n] = x
+    xd = _hip.to_device(big)[:, off:off + n]
+    assert xd.stride(0) == off + n + pad
+    np.testing.assert_array_equal(C.channel_means_device(xd).cpu().numpy(), x.mean(1))
+    np.testing.assert_array_equal(np.sqrt(C.channel_variances_device(xd).cpu().numpy()), np.std(x, axis=1))
+    bad = np.zeros(x.shape[0], bool)
+    bad[[2, 30]] = True
+    out, bins = C.renormalize_device(xd, badchans_mask=bad, cut_outliers=True)
+    np.testing.assert_array_equal(out.cpu().numpy(), co.renormalize(x, badchans_mask=bad, cut_outliers=True))
+    del out
+    torch.cuda.empty_cache()
