@@ -140,6 +140,16 @@ int pu_gaussian_filter1d(const double *x, int64_t n, const double *weights, int6
 /* factor[t] = numerator / x[t] (clean.py:80). */
 int pu_ratio(double numerator, const double *x, int64_t n, double *out, void *stream);
 
+/* np.median of a float64 device series (clean.py:80 ``np.median(lc_smooth)``) into
+ * out[0] on the device, bit-exact: radix select of the two middle order statistics,
+ * numpy's mean of them; NaN if any element is NaN.  ws: pu_median_workspace_bytes(),
+ * 8-byte aligned. */
+size_t pu_median_workspace_bytes(void);
+int pu_median(const double *x, int64_t n, double *out, void *ws, size_t ws_bytes, void *stream);
+
+/* factor[t] = numerator[0] / x[t] with the numerator in device memory (clean.py:80). */
+int pu_ratio_dev(const double *numerator, const double *x, int64_t n, double *out, void *stream);
+
 /* renormalize_data apply pass (clean.py:81-94): out[c][t] = bad[c] ? 0 :
  * (f64(x[c][t]) * factor[t] - spec[c]) / spec[c]; if col_means != NULL it also
  * writes the sequential column mean of ``out`` (the cut_outliers light curve). */

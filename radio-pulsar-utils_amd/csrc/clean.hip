@@ -409,6 +409,145 @@ __global__ void zero_cols_kernel(double *out, int64_t nrows, int64_t ld, const i
         if (k < ncols) out[rr * ld + cols[k]] = 0.0;
 }
 
+// ---------------------------------------------------------------- median
+// np.median of a float64 series on the device (clean.py:80), so the factor pass
+// does not wait on a host round trip.  Radix select over order-preserving 64-bit
+// keys: six digit passes (11,11,11,11,11,9 bits, high to low) narrow the key
+// prefixes of the two order statistics numpy averages (k = n/2-1 and n/2 for even
+// n, n/2 twice for odd n).  Each pass is a histogram kernel (LDS bins, one global
+// atomic add per non-empty bin and workgroup) plus a one-workgroup select kernel
+// that scans the bins and extends the prefix.  The result is numpy's mean of the
+// two values, add.reduce order: (0 + ((0 + a) + b)) / 2; any NaN gives NaN.
+constexpr int kMedBitsMax = 11;
+constexpr int kMedBins = 1 << kMedBitsMax;
+constexpr int kMedPasses = 6;
+
+struct MedState {
+    uint64_t prefix[2];
+    int64_t k[2];
+    uint32_t nan;
+    uint32_t pad;
+};
+
+__host__ __device__ constexpr int med_shift(int p) { return 64 - kMedBitsMax * (p + 1) > 0 ? 64 - kMedBitsMax * (p + 1) : 0; }
+__host__ __device__ constexpr int med_bits(int p) { return 64 - kMedBitsMax * p - med_shift(p); }
+
+__device__ __forceinline__ uint64_t order_key(double d)
+{
+    const uint64_t u = static_cast<uint64_t>(__double_as_longlong(d));
+    return (u >> 63) ? ~u : (u | (uint64_t(1) << 63));
+}
+
+__device__ __forceinline__ double key_value(uint64_t k)
+{
+    const uint64_t u = (k >> 63) ? (k & ~(uint64_t(1) << 63)) : ~k;
+    return __longlong_as_double(static_cast<long long>(u));
+}
+
+__global__ void median_init_kernel(MedState *st, uint32_t *hist, int64_t n)
+{
+    const int t = threadIdx.x;
+    if (t == 0) {
+        st->prefix[0] = st->prefix[1] = 0;
+        st->k[0] = (n % 2 == 0) ? n / 2 - 1 : n / 2;
+        st->k[1] = n / 2;
+        st->nan = 0;
+    }
+    for (int i = t; i < 2 * kMedBins; i += blockDim.x) hist[i] = 0;
+}
+
+__global__ void __launch_bounds__(256)
+median_hist_kernel(const double *__restrict__ x, int64_t n, MedState *st, uint32_t *hist, int pass)
+{
+    __shared__ uint32_t h[2][kMedBins];
+    for (int i = threadIdx.x; i < 2 * kMedBins; i += 256) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const int shift = med_shift(pass), bits = med_bits(pass);
+    const uint64_t dmask = (uint64_t(1) << bits) - 1;
+    const int hs = shift + bits;  // bits above the digit must match the prefix
+    const uint64_t p0 = st->prefix[0], p1 = st->prefix[1];
+    uint32_t nans = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const double d = x[i];
+        if (d != d) {
+            ++nans;
+            continue;
+        }
+        const uint64_t k = order_key(d);
+        const uint32_t dig = (uint32_t)((k >> shift) & dmask);
+        if (hs >= 64 || (k >> hs) == (p0 >> hs)) atomicAdd(&h[0][dig], 1u);
+        if (hs >= 64 || (k >> hs) == (p1 >> hs)) atomicAdd(&h[1][dig], 1u);
+    }
+    if (pass == 0 && nans) atomicAdd(&st->nan, nans);
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * kMedBins; i += 256) {
+        const uint32_t c = (&h[0][0])[i];
+        if (c) atomicAdd(&hist[i], c);
+    }
+}
+
+// One workgroup: per target, thread t owns bins [8t, 8t+8); an exclusive scan of
+// the 256 partial counts finds the bin holding rank k; the bins are cleared for
+// the next pass.
+__global__ void __launch_bounds__(256) median_select_kernel(MedState *st, uint32_t *hist, int pass)
+{
+    __shared__ uint32_t scan[256];
+    const int t = threadIdx.x;
+    const int shift = med_shift(pass);
+    for (int j = 0; j < 2; ++j) {
+        uint32_t *hj = hist + j * kMedBins;
+        uint32_t c[8], sum = 0;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            c[b] = hj[8 * t + b];
+            sum += c[b];
+        }
+        scan[t] = sum;
+        __syncthreads();
+        for (int off = 1; off < 256; off <<= 1) {
+            const uint32_t v = t >= off ? scan[t - off] : 0;
+            __syncthreads();
+            scan[t] += v;
+            __syncthreads();
+        }
+        const int64_t k = st->k[j];
+        const int64_t before = (int64_t)scan[t] - sum;
+        __syncthreads();
+        if (k >= before && k < before + (int64_t)sum) {
+            int64_t r = k - before;
+            int b = 0;
+            while (r >= (int64_t)c[b]) r -= c[b++];
+            st->prefix[j] |= (uint64_t)(8 * t + b) << shift;
+            st->k[j] = r;
+        }
+#pragma unroll
+        for (int b = 0; b < 8; ++b) hj[8 * t + b] = 0;
+        __syncthreads();
+    }
+}
+
+__global__ void median_final_kernel(const MedState *st, int64_t n, double *out)
+{
+    if (st->nan) {
+        out[0] = __longlong_as_double(0x7ff8000000000000ll);
+        return;
+    }
+    const double a = key_value(st->prefix[0]);
+    if (n % 2 == 0) {
+        const double b = key_value(st->prefix[1]);
+        out[0] = (0.0 + ((0.0 + a) + b)) / 2.0;
+    } else {
+        out[0] = (0.0 + (0.0 + a)) / 1.0;
+    }
+}
+
+__global__ void ratio_dev_kernel(const double *__restrict__ num, const double *__restrict__ x, int64_t n,
+                                 double *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = num[0] / x[i];
+}
+
 template <typename Tin, typename Ta, int MODE>
 int row_sums_t(const void *x, int64_t nrows, int64_t n, int64_t ld, const void *center, const double *scale,
                double divisor, void *out, void *ws, hipStream_t s)
@@ -622,6 +761,34 @@ int pu_renorm_apply(const void *x, int dtype, int64_t nchan, int64_t n, int64_t 
     default: pu::set_error("pu_renorm_apply: unsupported dtype %d", dtype); return PU_EUNSUPPORTED;
     }
     return pu::launch_check("apply_kernel");
+}
+
+size_t pu_median_workspace_bytes(void) { return sizeof(MedState) + 2 * kMedBins * sizeof(uint32_t); }
+
+int pu_median(const double *x, int64_t n, double *out, void *ws, size_t ws_bytes, void *stream)
+{
+    PU_REQUIRE(x && out && n > 0, "pu_median: bad arguments");
+    PU_REQUIRE(ws && ws_bytes >= pu_median_workspace_bytes(), "pu_median: workspace too small");
+    PU_REQUIRE(reinterpret_cast<uintptr_t>(ws) % 8 == 0, "pu_median: workspace not 8-byte aligned");
+    hipStream_t s = pu::as_stream(stream);
+    MedState *st = reinterpret_cast<MedState *>(ws);
+    uint32_t *hist = reinterpret_cast<uint32_t *>(st + 1);
+    hipLaunchKernelGGL(median_init_kernel, dim3(1), dim3(256), 0, s, st, hist, n);
+    const unsigned grid = std::min<int64_t>(1024, std::max<int64_t>(1, (n + 255) / 256));
+    for (int p = 0; p < kMedPasses; ++p) {
+        hipLaunchKernelGGL(median_hist_kernel, dim3(grid), dim3(256), 0, s, x, n, st, hist, p);
+        hipLaunchKernelGGL(median_select_kernel, dim3(1), dim3(256), 0, s, st, hist, p);
+    }
+    hipLaunchKernelGGL(median_final_kernel, dim3(1), dim3(1), 0, s, st, n, out);
+    return pu::launch_check("median_kernels");
+}
+
+int pu_ratio_dev(const double *numerator, const double *x, int64_t n, double *out, void *stream)
+{
+    PU_REQUIRE(numerator && x && out && n > 0, "pu_ratio_dev: bad arguments");
+    hipLaunchKernelGGL(ratio_dev_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, pu::as_stream(stream), numerator, x,
+                       n, out);
+    return pu::launch_check("ratio_dev_kernel");
 }
 
 int pu_zero_columns(double *out, int64_t nrows, int64_t ld, const int64_t *cols, int64_t ncols, void *stream)

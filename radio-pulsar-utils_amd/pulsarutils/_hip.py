@@ -41,6 +41,9 @@ SIGNATURES = {
     "pu_col_means": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp]),
     "pu_gaussian_filter1d": (_i32, [_vp, _i64, _vp, _i64, _vp, _vp]),
     "pu_ratio": (_i32, [_f64, _vp, _i64, _vp, _vp]),
+    "pu_median_workspace_bytes": (_sz, []),
+    "pu_median": (_i32, [_vp, _i64, _vp, _vp, _sz, _vp]),
+    "pu_ratio_dev": (_i32, [_vp, _vp, _i64, _vp, _vp]),
     "pu_renorm_apply": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
     "pu_zero_columns": (_i32, [_vp, _i64, _i64, _vp, _i64, _vp]),
     "pu_rebin_time": (_i32, [_vp, _i32, _i64, _i64, _i64, _i64, _vp, _vp]),

@@ -83,6 +83,18 @@ def channel_variances_device(x, means=None):
     return _row_sums(x, 1, center=means, divisor=x.shape[1])
 
 
+def median_device(x):
+    """``np.median`` of a 1-D float64 device tensor, as a 1-element device tensor
+    (radix select on the GPU; no host round trip)."""
+    t = _hip.torch()
+    lib = _hip.lib()
+    out = t.empty(1, dtype=t.float64, device=x.device)
+    ws = t.empty(lib.pu_median_workspace_bytes(), dtype=t.uint8, device=x.device)
+    _hip.check(lib.pu_median(_hip.ptr(x), x.numel(), _hip.ptr(out), _hip.ptr(ws), ws.numel(), _hip.stream_ptr()),
+               "pu_median")
+    return out
+
+
 def _host(t):
     return t.detach().cpu().numpy()
 
@@ -125,7 +137,8 @@ def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=
     """renormalize_data on a device tensor; returns (float64 device tensor, bad_bins or None).
 
     Passes (clean.py:73-105): zero-DM light curve over good channels (column means,
-    rows in order) -> gaussian_filter (GPU, scipy's order) -> host median -> factor
+    rows in order) -> gaussian_filter (GPU, scipy's order) -> median (GPU radix
+    select) -> factor
     -> per-channel mean of x*factor (numpy pairwise order) -> (x*f - mu)/mu with bad
     channels zeroed [+ its column mean] -> host uniform_filter1d(16) thresholds ->
     zero the bad time bins.
@@ -149,9 +162,9 @@ def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=
     smooth = t.empty(n, dtype=t.float64, device=dev)
     _hip.check(lib.pu_gaussian_filter1d(_hip.ptr(lc), n, _hip.ptr(dw), radius, _hip.ptr(smooth), s),
                "pu_gaussian_filter1d")
-    med = float(np.median(_host(smooth)))
+    med = median_device(smooth)
     factor = t.empty(n, dtype=t.float64, device=dev)
-    _hip.check(lib.pu_ratio(med, _hip.ptr(smooth), n, _hip.ptr(factor), s), "pu_ratio")
+    _hip.check(lib.pu_ratio_dev(_hip.ptr(med), _hip.ptr(smooth), n, _hip.ptr(factor), s), "pu_ratio_dev")
     spec = _row_sums(x, 2, scale=factor, divisor=n)
     if out is None:
         out = t.empty((nchan, n), dtype=t.float64, device=dev)

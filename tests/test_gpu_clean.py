@@ -101,3 +101,25 @@ def test_clean_strided_views(gpu, dt, n, pad, off):
     np.testing.assert_array_equal(out.cpu().numpy(), co.renormalize(x, badchans_mask=bad, cut_outliers=True))
     del out
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 8, 1001, 4096, 262144, 262145])
+def test_median_device_matches_numpy(gpu, n):
+    """np.median (clean.py:80) by device radix select: random, tied, signed-zero,
+    infinite and NaN series, odd and even lengths."""
+    from pulsarutils import _hip
+    rng = np.random.default_rng(n)
+    cases = [rng.standard_normal(n) * 1e3,
+             rng.integers(-3, 4, n).astype(np.float64),             # heavy ties
+             np.where(rng.random(n) < 0.5, -0.0, 0.0),                # signed zeros only
+             np.concatenate([rng.standard_normal(n - 1), [np.inf]]),
+             np.abs(rng.standard_normal(n)) + 1.0]
+    if n > 2:
+        nan = rng.standard_normal(n)
+        nan[n // 3] = np.nan
+        cases.append(nan)
+    for a in cases:
+        got = C.median_device(_hip.to_device(a)).cpu().numpy()[0]
+        want = np.median(a)
+        assert np.array_equal(np.array([got]), np.array([want]), equal_nan=True), (n, got, want)
+        assert np.signbit(got) == np.signbit(want)
