@@ -526,7 +526,16 @@ struct SubCfg {
 };
 using SubWide = SubCfg<16, 8, 8>;   // 128 trials x 512 samples, one workgroup per CU (160 KiB LDS)
 using SubPair = SubCfg<8, 16, 4>;   // 128 trials x 256 samples, two workgroups per CU (80 KiB each)
-enum SubShape { SUB_WIDE = 0, SUB_PAIR = 1 };
+using SubTall = SubCfg<16, 16, 4>;  // 256 trials x 256 samples, one workgroup per CU (160 KiB LDS)
+enum SubShape { SUB_WIDE = 0, SUB_PAIR = 1, SUB_TALL = 2 };
+
+template <class F>
+auto with_shape(int shape, F &&f)
+{
+    if (shape == SUB_PAIR) return f(SubPair{});
+    if (shape == SUB_TALL) return f(SubTall{});
+    return f(SubWide{});
+}
 
 // Slot record (int32): slot length (elements, <= TT + spread + 1), copy-0 byte offset in
 // the slot area, first channel, channels in the group, then the G sources of element
@@ -1054,7 +1063,7 @@ int launch_sub_g(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t 
 template <typename Tin>
 int launch_sub_shape(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
 {
-    return p->shape == SUB_PAIR ? launch_sub_g<SubPair, Tin>(p, a, plane, s) : launch_sub_g<SubWide, Tin>(p, a, plane, s);
+    return with_shape(p->shape, [&](auto c) { return launch_sub_g<decltype(c), Tin>(p, a, plane, s); });
 }
 
 int dispatch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
@@ -1238,9 +1247,9 @@ struct SubSlot {
 int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
 {
     const int64_t nchan = p->nchan, n = p->n, ndm = p->ndm;
-    const int W = shape == SUB_PAIR ? SubPair::W : SubWide::W;
-    const int D = shape == SUB_PAIR ? SubPair::D : SubWide::D;
-    const int64_t TT = shape == SUB_PAIR ? SubPair::TT : SubWide::TT;
+    const int W = with_shape(shape, [](auto c) { return decltype(c)::W; });
+    const int D = with_shape(shape, [](auto c) { return decltype(c)::D; });
+    const int64_t TT = with_shape(shape, [](auto c) { return (int64_t)decltype(c)::TT; });
     const int64_t T = (int64_t)W * D;
     const int ngroups = (int)((nchan + G - 1) / G);
     const bool dma = p->dtype == PU_F32;
@@ -1582,9 +1591,10 @@ int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int
     p->ntt = (int)((n + p->TT - 1) / p->TT);
 
     // LDS budget per workgroup (channel / subband mode); PU_LDS_BUDGET_KB overrides (tuning)
-    // subband workgroup shape: PU_SUB_SHAPE 0 = wide (1 WG/CU), 1 = pair (2 WGs/CU)
+    // subband workgroup shape: PU_SUB_SHAPE 0 = wide (1 WG/CU), 1 = pair (2 WGs/CU),
+    // 2 = tall (256 trials x 256 samples, 1 WG/CU)
     int shape = SUB_WIDE;
-    if (const char *env = getenv("PU_SUB_SHAPE")) shape = atoi(env) == 1 ? SUB_PAIR : SUB_WIDE;
+    if (const char *env = getenv("PU_SUB_SHAPE")) shape = std::clamp(atoi(env), 0, 2);
     size_t budget = kLdsBudget, sub_budget = shape == SUB_PAIR ? 80 * 1024 : 160 * 1024;
     if (const char *env = getenv("PU_LDS_BUDGET_KB")) budget = sub_budget = (size_t)std::max(8, atoi(env)) * 1024;
     // group size: explicit, else PU_GROUP, else 4; float32 accumulation only (the
@@ -1651,7 +1661,7 @@ size_t pu_plan_workspace_bytes(const pu_plan *p)
 int pu_plan_info(const pu_plan *p, int64_t *info, int n)
 {
     if (!p || !info) return 0;
-    const int64_t v[] = {p->ndm, p->ndt, p->ntt, p->group > 1 ? (p->shape == SUB_PAIR ? SubPair::T : SubWide::T) : kTPT, p->TT, p->ncc,
+    const int64_t v[] = {p->ndm, p->ndt, p->ntt, p->group > 1 ? with_shape(p->shape, [](auto c) { return decltype(c)::T; }) : kTPT, p->TT, p->ncc,
                          p->row_stride, (int64_t)p->lds_bytes, kVariants[p->variant].acc_f64, p->max_spread,
                          p->group, p->nslots_total, p->nstages, (int64_t)p->slot_bytes, p->raw_stride,
                          p->exec_adds, p->lds_traffic};

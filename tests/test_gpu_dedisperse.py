@@ -177,10 +177,12 @@ def test_plane_subband_small_lds_budget(gpu, dt, monkeypatch):
             assert np.all(np.abs(plane[k] - ref) <= f32_bound(x, sh[k])), k
 
 
+@pytest.mark.parametrize("shape", ["1", "2"])
 @pytest.mark.parametrize("dt", ["u8", "f32"])
-def test_plane_subband_pair_shape(gpu, dt, monkeypatch):
-    """The two-workgroups-per-CU subband shape (PU_SUB_SHAPE=1: 8 waves x 16 trials, time
-    tile 256) against the oracle, ragged N and a partial last group (nchan % 4 != 0)."""
+def test_plane_subband_pair_shape(gpu, dt, shape, monkeypatch):
+    """The time-tile-256 subband shapes (PU_SUB_SHAPE=1 pair: 8 waves x 16 trials, two
+    workgroups per CU; 2 tall: 16 waves x 16 trials) against the oracle, ragged N and a
+    partial last group (nchan % 4 != 0)."""
     c = CONFIGS["C2"]
     rng = np.random.default_rng(33)
     nchan, n = 130, 20000 + 37
@@ -188,7 +190,7 @@ def test_plane_subband_pair_shape(gpu, dt, monkeypatch):
     x = x.astype(np.uint8) if dt == "u8" else x.astype(np.float32)
     dms = np.linspace(0.0, 60.0, 150)
     sh = _hip.shift_table(nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
-    monkeypatch.setenv("PU_SUB_SHAPE", "1")
+    monkeypatch.setenv("PU_SUB_SHAPE", shape)
     info = {}
     plane = _plane(x, sh, "native", 4, info)
     assert info["group"] == 4 and info["time_tile"] == 256, info
