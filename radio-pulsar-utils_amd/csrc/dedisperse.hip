@@ -546,7 +546,7 @@ __host__ __device__ constexpr int slot_stride(int G) { return G <= 4 ? 8 : 16; }
 struct SubArgs {
     DedispArgs o;           // data, ld, nchan, n, ndt, ntt, small_n; plane / partials
     int32_t ngroups;
-    int32_t raw_stride;     // floats per staged channel row (DMA mode)
+    int32_t raw_stride;     // elements per staged channel row (DMA mode; bytes for 8-bit rows)
     int32_t zero_len;       // floats of the zero row at LDS offset 0 (DMA mode, partial groups)
     int32_t lds_bytes;      // dynamic LDS size: a stage's raw rows end here
     int32_t skip;           // tuning ablation (PU_SUB_SKIP; results invalid): 1 build, 2 sum, 4 DMA
@@ -668,14 +668,47 @@ __device__ __forceinline__ void dma_row_f32(unsigned char *dst, const float *row
     }
 }
 
-template <class C, typename Tin, int G, bool PLANE, bool STATS>
+// LDS-DMA of one 8-bit channel-row window [start, start + cover) mod n into dst, start
+// and n multiples of 4 (the planner folds each row's misalignment into the slot
+// sources): 1 KiB pieces while contiguous, per-lane modular dwords if it wraps.
+__device__ __forceinline__ void dma_row_u8(unsigned char *dst, const unsigned char *row, int start, int cover_bytes,
+                                           int n, bool small_n, int lane)
+{
+    if (!small_n && start + cover_bytes <= n) {
+        const unsigned char *src = row + start;
+        int off = 0;
+        for (; off + 1024 <= cover_bytes; off += 1024)
+            __builtin_amdgcn_global_load_lds((const void *)(src + off + 16 * lane),
+                                             (__attribute__((address_space(3))) void *)(dst + off), 16, 0, 0);
+        for (; off < cover_bytes; off += 256)
+            __builtin_amdgcn_global_load_lds((const void *)(src + off + 4 * lane),
+                                             (__attribute__((address_space(3))) void *)(dst + off), 4, 0, 0);
+    } else {
+        const int nd = n >> 2;
+        for (int off = 0; off < cover_bytes; off += 256) {
+            int idx = (start >> 2) + (off >> 2) + lane;
+            if (small_n) {
+                idx %= nd;
+            } else {
+                idx = idx >= nd ? idx - nd : idx;
+            }
+            __builtin_amdgcn_global_load_lds((const void *)(row + 4 * idx),
+                                             (__attribute__((address_space(3))) void *)(dst + off), 4, 0, 0);
+        }
+    }
+}
+
+// DMA8: 8-bit rows staged by LDS-DMA as bytes (plans with n % 4 == 0); otherwise 8-bit
+// and float64 builds read global memory.
+template <class C, typename Tin, int G, bool PLANE, bool STATS, bool DMA8>
 __global__ void __launch_bounds__(C::THREADS, 4)
 dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__restrict__ tile_stages,
                   const i32x4 *__restrict__ stages, const int32_t *__restrict__ slots,
                   const int32_t *__restrict__ base_tab, const uint32_t *__restrict__ rec_tab)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr bool kDma = std::is_same<Tin, float>::value;
+    constexpr bool kDma = std::is_same<Tin, float>::value || (DMA8 && std::is_same<Tin, uint8_t>::value);
+    constexpr int EB = std::is_same<Tin, float>::value ? 4 : 1;  // bytes per staged raw element
     constexpr int W = C::W, D = C::D, K = C::K, TT = C::TT;
     constexpr int MS = slot_stride(G);
     // chunks of 64 per build pass: one pass at a plan grid's spread when G x U values fit
@@ -703,6 +736,7 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
     const uint32_t smem_addr = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char *)smem;
     const uint32_t lds_base = smem_addr;  // slot records hold absolute LDS offsets
     const float *raw_lds = reinterpret_cast<const float *>(smem);
+    const unsigned char *raw_lds8 = smem;
 
     float acc[D][K];
 #pragma unroll
@@ -725,20 +759,26 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
         const int nc = min(st.y * G, o.nchan) - c0;
         // the stage's rows end at the top of LDS (the host packs stages so that they never
         // overlap the previous stage's slots, which are summed while these rows land)
-        unsigned char *raw = smem + a.lds_bytes - ((nc * a.raw_stride * 4 + 255) & ~255);
-        const int cover_bytes = (tile.z * 4 + 255) & ~255;
+        unsigned char *raw = smem + a.lds_bytes - ((nc * a.raw_stride * EB + 255) & ~255);
+        const int cover_bytes = (tile.z * EB + 255) & ~255;
         for (int ci = wave; ci < nc; ci += W) {
             const int c = c0 + ci;
             int start = (ci == wave ? base0 : ld_uniform(base_t + c)) + t0;
             if (start >= n) start -= n;
-            dma_row_f32(raw + ci * a.raw_stride * 4,
-                        reinterpret_cast<const float *>(data) + (size_t)c * (size_t)o.ld, start, cover_bytes, n,
-                        small_n, lane);
+            if constexpr (EB == 4)
+                dma_row_f32(raw + ci * a.raw_stride * 4,
+                            reinterpret_cast<const float *>(data) + (size_t)c * (size_t)o.ld, start, cover_bytes, n,
+                            small_n, lane);
+            else
+                dma_row_u8(raw + ci * a.raw_stride, reinterpret_cast<const unsigned char *>(data) + (size_t)c * (size_t)o.ld,
+                           start, cover_bytes, n, small_n, lane);
         }
     };
 
     auto load = [&](const meta_t &m, int q, int i) -> float {
-        if constexpr (kDma) {
+        if constexpr (kDma && EB == 1) {
+            return static_cast<float>(raw_lds8[m[4 + q] + i]);  // ds_read_u8
+        } else if constexpr (kDma) {
             return raw_lds[m[4 + q] + i];  // past the slot only for masked lanes (row padding)
         } else {
             int pos = m[4 + q] + t0 + i;
@@ -963,6 +1003,7 @@ struct pu_plan {
     // subband mode (group > 1): per tile {first, count, raw row length, copy bytes},
     // stages {group begin, group end, item begin, item end}, build items, window records
     int group = 1, ngroups = 0, nslots_total = 0, raw_stride = 0, shape = SUB_WIDE;
+    int dma8 = 0;  // subband plan stages 8-bit rows by LDS-DMA (rows must be 4-byte aligned)
     size_t slot_bytes = 0, zero_len = 0;
     int64_t exec_adds = 0, lds_traffic = 0;  // per launch (measurement: bench.py roofline)
     int64_t nstages = 0;
@@ -1032,20 +1073,20 @@ int launch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
     sa.lds_bytes = (int32_t)p->lds_bytes;
     if (const char *env = getenv("PU_SUB_SKIP")) sa.skip = atoi(env);
     const dim3 grid((unsigned)((int64_t)p->ndt * p->ntt)), block(C::THREADS);
-    if (plane) {
-        auto kern = dedisp_sub_kernel<C, Tin, G, true, false>;
+    auto go = [&](auto kern) {
         int rc = ensure_lds(kern, p->lds_bytes);
         if (rc) return rc;
         hipLaunchKernelGGL(kern, grid, block, p->lds_bytes, s, sa, p->d_tiles, p->d_tile_stages, p->d_stages,
                            p->d_slots, p->d_base, p->d_recs);
-    } else {
-        auto kern = dedisp_sub_kernel<C, Tin, G, false, true>;
-        int rc = ensure_lds(kern, p->lds_bytes);
-        if (rc) return rc;
-        hipLaunchKernelGGL(kern, grid, block, p->lds_bytes, s, sa, p->d_tiles, p->d_tile_stages, p->d_stages,
-                           p->d_slots, p->d_base, p->d_recs);
+        return pu::launch_check("dedisp_sub_kernel");
+    };
+    if constexpr (std::is_same<Tin, uint8_t>::value) {
+        if (p->dma8)
+            return plane ? go(dedisp_sub_kernel<C, Tin, G, true, false, true>)
+                         : go(dedisp_sub_kernel<C, Tin, G, false, true, true>);
     }
-    return pu::launch_check("dedisp_sub_kernel");
+    return plane ? go(dedisp_sub_kernel<C, Tin, G, true, false, false>)
+                 : go(dedisp_sub_kernel<C, Tin, G, false, true, false>);
 }
 
 template <class C, typename Tin>
@@ -1252,17 +1293,25 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     const int64_t TT = with_shape(shape, [](auto c) { return (int64_t)decltype(c)::TT; });
     const int64_t T = (int64_t)W * D;
     const int ngroups = (int)((nchan + G - 1) / G);
-    const bool dma = p->dtype == PU_F32;
+    // 8-bit rows are staged as bytes by LDS-DMA when every row window starts on a dword
+    // (n % 4 == 0; the row's misalignment base % 4 is folded into the slot sources)
+    bool dma8 = p->dtype == PU_U8 && n % 4 == 0;
+    if (const char *env = getenv("PU_U8_DMA")) dma8 = dma8 && atoi(env) != 0;
+    const bool dma = p->dtype == PU_F32 || dma8;
+    const int64_t eb = dma8 ? 1 : 4;  // bytes per staged raw element
     // a stage's raw rows (DMA mode) and its slots share the LDS budget; a stage holds
     // whole groups.  The zero row (DMA mode, partial last group) sits at the end.
     const bool partial = dma && nchan % G != 0;
     const int64_t lds_cap = (int64_t)budget;
     auto S = [&](int64_t d, int64_t c) { return shifts[d * nchan + c]; };
-    auto raw_stride_of = [&](int64_t spread) { return (TT + spread + 1 + 63) / 64 * 64; };
+    // elements per staged row: whole 256-byte DMA pieces for 8-bit rows (+3 misalignment)
+    auto raw_stride_of = [&](int64_t spread) {
+        return dma8 ? (TT + spread + 1 + 3 + 255) / 256 * 256 : (TT + spread + 1 + 63) / 64 * 64;
+    };
     // slot copy: len = TT + span + 1 elements + 1 padding float (copy 1's element -1)
     auto copy_of = [&](int64_t span) { return (TT + span + 2 + 63) / 64 * 64 * 4; };
-    auto zero_bytes = [&](int64_t stride) { return partial ? ((stride + 64) * 4 + 255) / 256 * 256 : 0; };
-    auto raw_bytes = [&](int64_t chans, int64_t stride) { return dma ? (chans * stride * 4 + 255) / 256 * 256 : 0; };
+    auto zero_bytes = [&](int64_t stride) { return partial ? ((stride + 64) * eb + 255) / 256 * 256 : 0; };
+    auto raw_bytes = [&](int64_t chans, int64_t stride) { return dma ? (chans * stride * eb + 255) / 256 * 256 : 0; };
     // one group's rows, `slots` slots and the zero row fit the budget
     auto group_fits = [&](int64_t spread, int64_t slots, int64_t span) {
         const int64_t rs = raw_stride_of(spread);
@@ -1392,10 +1441,14 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     std::vector<uint32_t> rec((size_t)ndt * ngroups * W * D);
     std::vector<int64_t> slot_local((size_t)ngroups), slot_base((size_t)ngroups);
     int64_t prev_slots = 0;
-    // float offset of a stage's first raw row: its rows end at the top of LDS
+    // element offset of a stage's first raw row: its rows end at the top of LDS
     auto raw_top_f = [&](int g0, int g1) {
         const int64_t nc = std::min<int64_t>((int64_t)g1 * G, nchan) - (int64_t)g0 * G;
-        return (lds_cap - raw_bytes(nc, raw_stride)) / 4;
+        return (lds_cap - raw_bytes(nc, raw_stride)) / eb;
+    };
+    auto base_of = [&](int64_t smin_c) {
+        int64_t b = smin_c % n;
+        return b < 0 ? b + n : b;
     };
     int64_t slot_used = 0, max_stage_chans = 0;
     int64_t adds_tile = 0, lds_tile = 0;  // per time tile, summed over DM tiles
@@ -1405,12 +1458,10 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
         const int64_t trials_run = (count[t] + D - 1) / D * D;  // active waves run all D trials
         adds_tile += trials_run * ngroups * TT;
         lds_tile += trials_run * ngroups * TT * 4;  // sum: one window read per trial and group
-        tiles[t] = i32x4{first[t], count[t], (int32_t)(TT + spread_t[t] + 1), (int32_t)cb};
+        const int64_t row_len = TT + spread_t[t] + 1 + (dma8 ? 3 : 0);  // staged elements per row
+        tiles[t] = i32x4{first[t], count[t], (int32_t)row_len, (int32_t)cb};
         if (dma)
-            for (int64_t c = 0; c < nchan; ++c) {
-                int64_t b = smin[c] % n;
-                base.push_back((int32_t)(b < 0 ? b + n : b));
-            }
+            for (int64_t c = 0; c < nchan; ++c) base.push_back((int32_t)(dma8 ? base_of(smin[c]) & ~int64_t(3) : base_of(smin[c])));
         tile_stages[t] = i32x2{(int32_t)stages.size(), 0};
         prev_slots = 0;
         int g = 0;
@@ -1444,7 +1495,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
                 for (const auto &sl : sls) {
                     const int64_t len = TT + (sl.hi - sl.lo) + 1;
                     adds_tile += len * gs;
-                    lds_tile += ((len + 63) / 64 * 64) * (dma ? 4 * G + 8 : 8);  // build reads + 2 writes
+                    lds_tile += ((len + 63) / 64 * 64) * (dma ? eb * G + 8 : 8);  // build reads + 2 writes
                     slotmeta.push_back((int32_t)len);
                     slotmeta.push_back((int32_t)(zr + used * 2 * cb));
                     slotmeta.push_back((int32_t)c0);
@@ -1455,7 +1506,8 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
                             // smallest shift of channel c0+k over the slot's trials
                             const int64_t sk = sl.lo + S(sl.d0, c0 + k) - S(sl.d0, c0);
                             if (dma) {
-                                src = raw_top_f(g, g_stop) + (chans + k) * raw_stride + (sk - smin[c0 + k]);
+                                src = raw_top_f(g, g_stop) + (chans + k) * raw_stride + (sk - smin[c0 + k]) +
+                                      (dma8 ? (base_of(smin[c0 + k]) & 3) : 0);
                             } else {
                                 src = sk % n;
                                 if (src < 0) src += n;
@@ -1470,7 +1522,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
             }
             stages.push_back(i32x4{g, g_end, s_begin, (int32_t)(slotmeta.size() / ms)});
             tile_stages[t][1]++;
-            if (dma) lds_tile += chans * ((TT + spread_t[t] + 1) * 4 + 255) / 256 * 256;  // DMA writes
+            if (dma) lds_tile += chans * ((row_len * eb + 255) / 256 * 256);  // DMA writes
             slot_used = std::max(slot_used, zr + used * 2 * cb);
             for (int gg = g; gg < g_end; ++gg) slot_base[gg] = zr;
             max_stage_chans = std::max(max_stage_chans, chans);
@@ -1514,7 +1566,8 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     p->row_stride = (int)raw_stride;
     p->max_spread = (int)max_spread;
     p->small_n = raw_stride + 2 > n ? 1 : 0;
-    p->zero_len = zr ? (size_t)(raw_stride + 64) : 0;
+    p->zero_len = zr ? (size_t)(((raw_stride + 64) * eb + 3) / 4) : 0;  // floats
+    p->dma8 = dma8 ? 1 : 0;
     p->slot_bytes = (size_t)slot_used;
     p->lds_bytes = (size_t)lds_total;
     p->nslots_total = (int)(slotmeta.size() / ms);
@@ -1675,6 +1728,8 @@ static int check_data(const pu_plan *p, const void *data, int64_t ld)
     PU_REQUIRE(p != nullptr, "plan is NULL");
     PU_REQUIRE(data != nullptr, "data is NULL");
     PU_REQUIRE(ld >= p->n, "ld %lld < nsamples %lld", (long long)ld, (long long)p->n);
+    PU_REQUIRE(!p->dma8 || (reinterpret_cast<uintptr_t>(data) % 4 == 0 && ld % 4 == 0),
+               "8-bit subband plan: rows must start on 4-byte boundaries (data %% 4 == 0, ld %% 4 == 0)");
     return PU_OK;
 }
 

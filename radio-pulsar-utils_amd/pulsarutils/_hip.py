@@ -186,10 +186,19 @@ class Plan:
         assert tuple(data.shape) == (self.nchan, self.nsamples), (tuple(data.shape), self.nchan, self.nsamples)
         assert dtype_code(data.dtype) == self.dtype_code
 
+    @staticmethod
+    def _rows_aligned(data):
+        """8-bit rows are staged by LDS-DMA in whole dwords: a view whose rows do not start
+        on 4-byte boundaries is copied once into a fresh (aligned, contiguous) tensor."""
+        if data.element_size() == 1 and (data.data_ptr() % 4 or data.stride(0) % 4):
+            return data.clone(memory_format=torch().contiguous_format)
+        return data
+
     def search(self, data, out=None, workspace=None, stream=None):
         """Launch the fused search; returns (max, std, snr, rebin) device tensors."""
         t = torch()
         self._check_data(data)
+        data = self._rows_aligned(data)
         dev = data.device
         if out is None:
             out = (t.empty(self.ndm, dtype=t.float64, device=dev), t.empty(self.ndm, dtype=t.float64, device=dev),
@@ -215,6 +224,7 @@ class Plan:
         """Dedispersed plane (ndm, nsamples) in the accumulation dtype."""
         t = torch()
         self._check_data(data)
+        data = self._rows_aligned(data)
         if plane is None:
             plane = t.empty((self.ndm, self.nsamples), dtype=t.float64 if self.acc_is_f64 else t.float32,
                             device=data.device)

@@ -315,3 +315,34 @@ def test_search_u8_bitexact_series_c3_slice(gpu):
     for k in range(len(idx)):
         np.testing.assert_array_equal(plane[k].astype(np.float64), oracle.dedisperse(x, sh[k]))
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("shape", ["0", "1", "2"])
+def test_plane_u8_dma_rows(gpu, shape, monkeypatch):
+    """8-bit rows staged by LDS-DMA (N % 4 == 0): bit-exact against the oracle and the
+    global-read build (PU_U8_DMA=0), with a partial last group, row misalignments
+    (base % 4 != 0), a padded row stride and a view whose rows are not 4-byte aligned."""
+    import torch
+    c = CONFIGS["C2"]
+    rng = np.random.default_rng(44)
+    nchan, n = 130, 20000
+    x = (rng.random((nchan, n)) * 60).astype(np.uint8)
+    dms = np.linspace(0.0, 60.0, 150)
+    sh = _hip.shift_table(nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
+    monkeypatch.setenv("PU_SUB_SHAPE", shape)
+    plan = _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, nchan, n, sh, group=4)
+    assert plan.info["group"] == 4, plan.info
+    xd = _hip.to_device(x)
+    plane = plan.dedisperse(xd).cpu().numpy()
+    for k in range(0, 150, 13):
+        np.testing.assert_array_equal(plane[k].astype(np.float64), oracle.dedisperse(x, sh[k]))
+    monkeypatch.setenv("PU_U8_DMA", "0")
+    ref = _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, nchan, n, sh, group=4).dedisperse(xd).cpu().numpy()
+    np.testing.assert_array_equal(plane, ref)
+    monkeypatch.delenv("PU_U8_DMA")
+    big = torch.zeros((nchan, n + 8), dtype=torch.uint8, device=xd.device)
+    big[:, 4:4 + n] = xd
+    np.testing.assert_array_equal(plan.dedisperse(big[:, 4:4 + n]).cpu().numpy(), plane)  # ld = n + 8
+    np.testing.assert_array_equal(plan.dedisperse(big[:, 1:1 + n].copy_(xd)).cpu().numpy(), plane)  # copied
+    g = plan.search(big[:, 1:1 + n])
+    torch.cuda.synchronize()
