@@ -47,6 +47,7 @@ def log(*a):
 
 def cpu_baseline(x_host, dms, cfg, ntrials, threads):
     import oracle
+    ntrials = min(ntrials, dms.size)
     sel = dms[np.linspace(0, dms.size - 1, ntrials).astype(int)]
     oracle.search(x_host[:, :4096], sel[:2], cfg.start_freq, cfg.bandwidth, cfg.tsamp, nthreads=threads)
     t0 = time.perf_counter()
@@ -54,8 +55,8 @@ def cpu_baseline(x_host, dms, cfg, ntrials, threads):
     dt = time.perf_counter() - t0
     return {"value": ntrials * cfg.nsamples / dt, "unit": "DM-trial samples/s", "cores": threads,
             "kind": "port",
-            "sample": f"{ntrials} of the {dms.size} C2 trials (evenly spaced), full 1024x2^20 float32 "
-                      f"filterbank, float64 oracle/dedisp_oracle.c (numba prange -> OpenMP), {dt:.1f} s"}
+            "sample": f"{ntrials} of the {dms.size} {cfg.name} trials (evenly spaced), full "
+                      f"{cfg.nchan}x2^{int(np.log2(cfg.nsamples))} {cfg.dtype} filterbank, float64 oracle/dedisp_oracle.c (numba prange -> OpenMP), {dt:.1f} s"}
 
 
 def load_pmc(workload):
