@@ -299,6 +299,38 @@ def test_search_full_size_sampled_trials(gpu, golden, name):
     np.testing.assert_array_equal(win.cpu().numpy()[idx], owin)
 
 
+def test_search_c3_full_size_u8(gpu):
+    """Maximum size (C3: 4096 x 2^22 uint8, 5000 trials, 17 GB in HBM): the full search
+    finds the injected pulse; for the first, best and last trial the dedispersed series
+    is bit-equal to the float64 C oracle (integer partial sums < 2^24 are exact in float32)
+    and the statistics match it within SURVEY §8a's 1e-5."""
+    import torch
+    from pulsarutils import synth
+    c = CONFIGS["C3"]
+    xd = synth.pulsar_filterbank_device(c)
+    dms = D.dedispersion_plan(c.nchan, c.dmmin, c.dmmax, c.start_freq, c.bandwidth, c.tsamp)
+    assert dms.size == 5000
+    (mx, sd, snr, win), _ = D.search_device(xd, dms, c.nchan, c.start_freq, c.bandwidth, c.tsamp)
+    torch.cuda.synchronize()
+    snr = snr.cpu().numpy()
+    best = int(np.argmax(snr))
+    assert abs(dms[best] - c.pulse_dm) < 0.5, (dms[best], c.pulse_dm)
+    idx = np.array([0, best, dms.size - 1])
+    sh = _hip.shift_table(c.nchan, dms[idx], c.start_freq, c.bandwidth, c.tsamp)
+    plane = _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, c.nchan, c.nsamples, sh).dedisperse(xd).cpu().numpy()
+    x = xd.cpu().numpy()
+    del xd
+    torch.cuda.empty_cache()
+    omx, osd, osnr, owin, dd = oracle.search(x, dms[idx], c.start_freq, c.bandwidth, c.tsamp,
+                                             nthreads=16, return_dedisp=True)
+    for k in range(idx.size):
+        np.testing.assert_array_equal(plane[k].astype(np.float64), dd[k])
+    np.testing.assert_allclose(snr[idx], osnr, rtol=1e-5)
+    np.testing.assert_allclose(sd.cpu().numpy()[idx], osd, rtol=1e-5)
+    np.testing.assert_allclose(mx.cpu().numpy()[idx], omx, rtol=1e-5)
+    np.testing.assert_array_equal(win.cpu().numpy()[idx], owin)
+
+
 def test_search_u8_bitexact_series_c3_slice(gpu):
     """uint8 C3-like slice: float32 accumulation is exact -> plane equals the float64 oracle."""
     import torch
