@@ -14,7 +14,10 @@ float32, float32 in float32 (stated tolerance) and float64 in float64 (bit-exact
 reference's dedispersed series.  The environment variable ``PULSARUTILS_ACC``
 changes the default.
 """
+import collections
+import hashlib
 import os
+import threading
 
 import numpy as np
 
@@ -117,8 +120,37 @@ def _prepare_data(data):
     return x
 
 
-def _plan_for(x, shifts, acc):
-    return _hip.Plan(_hip.dtype_code(x.dtype), acc, x.shape[0], x.shape[1], shifts)
+# Plans (tiling + device metadata) of recent calls, so repeated numpy-API calls on the same
+# shape and trial grid skip the host planner (~35 ms at C2).  A plan is read-only during a
+# launch (workspace and outputs are per call), so sharing one is safe.  The key holds the
+# planner's tuning variables, which are read when a plan is built.
+_PLAN_CACHE = collections.OrderedDict()
+_PLAN_CACHE_SIZE = 4
+_PLAN_LOCK = threading.Lock()
+_PLAN_ENV = ("PU_SUB_SHAPE", "PU_LDS_BUDGET_KB", "PU_GROUP", "PU_U8_DMA", "PU_SUB_SKIP")
+
+
+def _plan_for(x, shifts, acc, ident=None):
+    """Cached plan for ``x``'s shape/dtype.  ``shifts`` is the int64 shift table or a
+    callable producing it; ``ident`` (hashable) names the table cheaply (the trial grid
+    and band), so a cache hit never builds or hashes the table."""
+    if ident is None:
+        shifts = np.ascontiguousarray(shifts, dtype=np.int64)
+        ident = (hashlib.sha1(shifts.tobytes()).hexdigest(), shifts.shape)
+    key = (_hip.dtype_code(x.dtype), acc, x.shape[0], x.shape[1], x.device.index, ident,
+           tuple(os.environ.get(k) for k in _PLAN_ENV))
+    with _PLAN_LOCK:
+        plan = _PLAN_CACHE.get(key)
+        if plan is not None:
+            _PLAN_CACHE.move_to_end(key)
+            return plan
+    sh = shifts() if callable(shifts) else shifts
+    plan = _hip.Plan(key[0], acc, x.shape[0], x.shape[1], sh)
+    with _PLAN_LOCK:
+        _PLAN_CACHE[key] = plan
+        while len(_PLAN_CACHE) > _PLAN_CACHE_SIZE:
+            _PLAN_CACHE.popitem(last=False)
+    return plan
 
 
 def dedisperse(data, shifts, acc="f64"):
@@ -142,8 +174,11 @@ def search_device(data, trial_DMs, nchan, start_freq, bandwidth, sample_time, ac
     if int(nchan) != x.shape[0]:
         raise ValueError("nchan does not match data.shape[0]")
     if plan is None:
-        sh = _hip.shift_table(nchan, trial_DMs, start_freq, bandwidth, sample_time)
-        plan = _plan_for(x, sh, _acc_code(acc))
+        dms = np.ascontiguousarray(np.atleast_1d(np.asarray(trial_DMs, dtype=np.float64)))
+        ident = ("dm", hashlib.sha1(dms.tobytes()).hexdigest(), dms.size, float(start_freq),
+                 float(bandwidth), float(sample_time))
+        plan = _plan_for(x, lambda: _hip.shift_table(nchan, dms, start_freq, bandwidth, sample_time),
+                         _acc_code(acc), ident)
     return plan.search(x), plan
 
 

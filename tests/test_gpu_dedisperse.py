@@ -299,6 +299,30 @@ def test_search_full_size_sampled_trials(gpu, golden, name):
     np.testing.assert_array_equal(win.cpu().numpy()[idx], owin)
 
 
+def test_plan_cache_reuse(gpu, monkeypatch):
+    """Repeated numpy-API calls reuse the cached plan (same results); a different trial
+    grid or planner variable builds a new one."""
+    c = CONFIGS["C2"]
+    rng = np.random.default_rng(7)
+    x = rng.random((64, 4096)).astype(np.float32)
+    dms = np.linspace(0.0, 30.0, 40)
+    args = (64, c.start_freq, c.bandwidth, c.tsamp)
+    a = D._dedispersion_search(x, dms, *args)
+    _, p1 = D.search_device(x, dms, *args)
+    _, p2 = D.search_device(x, dms, *args)
+    assert p1 is p2
+    b = D._dedispersion_search(x, dms, *args)
+    for u, v in zip(a, b):
+        np.testing.assert_array_equal(u, v)
+    _, p3 = D.search_device(x, dms[:-1], *args)
+    assert p3 is not p1
+    monkeypatch.setenv("PU_SUB_SHAPE", "1")
+    _, p4 = D.search_device(x, dms, *args)
+    assert p4 is not p1
+    for u, v in zip(a, D._dedispersion_search(x, dms, *args)):
+        np.testing.assert_allclose(u, v, rtol=1e-5)
+
+
 def test_search_c3_full_size_u8(gpu):
     """Maximum size (C3: 4096 x 2^22 uint8, 5000 trials, 17 GB in HBM): the full search
     finds the injected pulse; for the first, best and last trial the dedispersed series
