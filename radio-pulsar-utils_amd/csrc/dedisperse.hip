@@ -1653,14 +1653,38 @@ int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int
     // group size: explicit, else PU_GROUP, else 4; float32 accumulation only (the
     // float64 modes keep the reference's sequential channel order)
     int G = group;
+    bool auto_g = false;
     if (G == 0) {
         G = 4;
         if (const char *env = getenv("PU_GROUP")) G = atoi(env);
+        else auto_g = !kVariants[v].acc_f64 && nchan > 8;
     }
     G = std::min(G, 8);
     if (kVariants[v].acc_f64) G = 1;
     while (G > 1 && G >= nchan) G >>= 1;
     int rc = PU_EUNSUPPORTED;
+    if (auto_g) {
+        // Default group size: plan G = 8 and G = 4 and keep the cheaper by the measured
+        // cost model: LDS bytes + 3.0e6 B-equivalent per (stage, time tile).
+        // G = 8 halves the LDS traffic at C3 (1240 vs 1328 ms) but its extra stages cost
+        // more than that at C2 (22.7 vs 18.4 ms) and C5.
+        auto cost = [](const pu_plan *q) { return (double)q->lds_traffic + 3.0e6 * (double)q->nstages * q->ntt; };
+        if (plan_sub(p, shifts, 8, shape, sub_budget) == PU_OK) {
+            const double c8 = cost(p);
+            reset_tables(p);
+            rc = plan_sub(p, shifts, 4, shape, sub_budget);
+            if (rc != PU_OK || cost(p) > c8) {
+                reset_tables(p);
+                rc = plan_sub(p, shifts, 8, shape, sub_budget);
+            }
+            if (rc == PU_OK) {
+                *out = p;
+                return PU_OK;
+            }
+        }
+        reset_tables(p);
+        rc = PU_EUNSUPPORTED;
+    }
     for (; G > 1 && rc == PU_EUNSUPPORTED; G >>= 1) {
         rc = plan_sub(p, shifts, G, shape, sub_budget);
         if (rc == PU_EUNSUPPORTED) reset_tables(p);
