@@ -299,6 +299,18 @@ def test_search_full_size_sampled_trials(gpu, golden, name):
     np.testing.assert_array_equal(win.cpu().numpy()[idx], owin)
 
 
+@pytest.mark.parametrize("name,group", [("C2", 4), ("C3", 8), ("C5", 4)])
+def test_default_group_cost_model(gpu, golden, name, group):
+    """With no explicit group the planner keeps the cheaper of G = 8 / G = 4 by its cost
+    model; at C2/C3/C5 that is the measured winner (profiles/r01_autog/)."""
+    c = CONFIGS[name]
+    dms = D.dedispersion_plan(c.nchan, c.dmmin, c.dmmax, c.start_freq, c.bandwidth, c.tsamp)
+    sh = _hip.shift_table(c.nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
+    code = {"u8": _hip.PU_U8, "f32": _hip.PU_F32}[c.dtype]
+    info = _hip.Plan(code, _hip.PU_ACC_NATIVE, c.nchan, c.nsamples, sh).info
+    assert info["group"] == group, info
+
+
 def test_plan_cache_reuse(gpu, monkeypatch):
     """Repeated numpy-API calls reuse the cached plan (same results); a different trial
     grid or planner variable builds a new one."""
