@@ -1669,18 +1669,28 @@ int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int
         // G = 8 halves the LDS traffic at C3 (1240 vs 1328 ms) but its extra stages cost
         // more than that at C2 (22.7 vs 18.4 ms) and C5.
         auto cost = [](const pu_plan *q) { return (double)q->lds_traffic + 3.0e6 * (double)q->nstages * q->ntt; };
-        if (plan_sub(p, shifts, 8, shape, sub_budget) == PU_OK) {
-            const double c8 = cost(p);
-            reset_tables(p);
-            rc = plan_sub(p, shifts, 4, shape, sub_budget);
-            if (rc != PU_OK || cost(p) > c8) {
-                reset_tables(p);
-                rc = plan_sub(p, shifts, 8, shape, sub_budget);
-            }
-            if (rc == PU_OK) {
-                *out = p;
-                return PU_OK;
-            }
+        // both candidates are built once (the G = 8 one in a second plan object)
+        pu_plan *q = new pu_plan();
+        q->dtype = p->dtype;
+        q->acc = p->acc;
+        q->variant = p->variant;
+        q->nchan = p->nchan;
+        q->n = p->n;
+        q->ndm = p->ndm;
+        q->K = p->K;
+        q->TT = p->TT;
+        q->ntt = p->ntt;
+        const bool ok8 = plan_sub(q, shifts, 8, shape, sub_budget) == PU_OK;
+        const bool ok4 = plan_sub(p, shifts, 4, shape, sub_budget) == PU_OK;
+        if (ok8 && (!ok4 || cost(p) > cost(q))) {
+            free_plan(p);
+            *out = q;
+            return PU_OK;
+        }
+        free_plan(q);
+        if (ok4) {
+            *out = p;
+            return PU_OK;
         }
         reset_tables(p);
         rc = PU_EUNSUPPORTED;
