@@ -69,9 +69,10 @@ typedef struct pu_plan pu_plan;
 int pu_plan_create(pu_plan **plan, int dtype, int acc, int64_t nchan, int64_t nsamples,
                    const int64_t *shifts, int64_t ndm);
 /* Same, choosing the float32-accumulation strategy: ``group`` = channels summed into
- * one exact partial-sum row per distinct relative-shift vector (DESIGN.md §4.2):
- * 0 = default (PU_GROUP env or 4, falling back to smaller groups / channel mode when
- * the trial grid does not suit it), 1 = channel mode, 2/4/8.  Float64
+ * one exact partial-sum row per distinct relative-shift vector (DESIGN.md §4.1):
+ * 0 = default (PU_GROUP env, else the cheaper of 8 and 4 by the planner's cost model,
+ * falling back to smaller groups / channel mode when the trial grid does not suit
+ * them), 1 = channel mode, 2/4/8.  Float64
  * accumulation always runs channel mode (the reference's channel order). */
 int pu_plan_create_grouped(pu_plan **plan, int dtype, int acc, int64_t nchan, int64_t nsamples,
                            const int64_t *shifts, int64_t ndm, int group);
