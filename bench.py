@@ -4,14 +4,22 @@ One "step" = one fused DM-trial search (pu_plan_search: shift-and-sum over all
 channels for every trial + the S/N epilogue + the per-trial finalize) over a
 1024-channel x 2^20-sample float32 filterbank resident in HBM, 1000 trials per GPU.
 
-N GPUs (one process each, torchrun): weak scaling.  The DM grid is N x 1000 trials,
-sharded contiguously (rank r owns trials [1000 r, 1000 (r+1))); the filterbank is
-generated on rank 0 and RCCL-broadcast over xGMI before timing (reported separately
-as broadcast_ms); each step ends with an all_gather of the per-trial statistics.
+Scaling (one process per GPU, torchrun; DM trials are independent, so there is no
+collective on the data path - DESIGN.md §5):
+* ``--scaling weak`` (default): the DM grid is N x ``ntrials`` trials, rank r owns
+  trials [r ntrials, (r+1) ntrials).
+* ``--scaling strong``: the config's own grid (C3: 5000 trials) is split contiguously
+  over the N ranks (C3 at N = 8: 625 trials per GPU).
+The filterbank is generated on rank 0 and RCCL-broadcast over xGMI before timing
+(``broadcast_ms``; chunked so the search of early time chunks overlaps the transfer
+of later ones: ``end_to_end_ms`` = broadcast + search of one step, pipelined); each
+step ends with an all_gather of the per-trial statistics.
 
 Prints ONE JSON line (rank 0) with the driver's contract fields plus ``roofline``
-(dominant kernel, HIP events on its launch stream) and ``cpu_baseline`` (the C
-oracle = a port of the reference's numba search, timed on a bounded trial sample).
+(dominant kernel, HIP events on its launch stream; HBM counter traffic from the PMC
+summary committed under profiles/), ``clean`` (the C4 cleaning pass, configs[3]) and
+``cpu_baseline`` (the C oracle = a port of the reference's numba search, OpenMP over
+trials, timed on a bounded trial sample on the host's cores).
 """
 import argparse
 import json
@@ -31,12 +39,15 @@ import torch.distributed as dist  # noqa: E402
 from pulsarutils import _hip, synth  # noqa: E402
 from pulsarutils.configs import CONFIGS  # noqa: E402
 from pulsarutils.dedispersion import dedispersion_plan  # noqa: E402
+from pulsarutils.parallel import shard_bounds  # noqa: E402
 
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
 HBM_PEAK_GBS = 8000.0
 # float32 vector peak is 157.3 TFLOP/s counting an FMA as 2 FLOP; an add is one FLOP
 # per lane-op, so the add-only ceiling is half of it: 256 CU x 128 lanes/clk x 2.4 GHz
 VALU_ADD_PEAK_TFLOPS = 78.6
+# float64 vector peak 78.6 TFLOP/s (FMA = 2 FLOP) -> 39.3 T float64 adds/s
+VALU_F64_ADD_PEAK_TFLOPS = 39.3
 # LDS: 256 B/clk/CU for ds_read_b64 (MI355X_MICROARCH.md §LDS) x 256 CUs x 2.4 GHz
 LDS_PEAK_TBPS = 157.3
 
@@ -45,7 +56,29 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads():
+    """Threads for the CPU baseline: every CPU this process may run on (its affinity
+    mask), capped by OMP_NUM_THREADS when the host sets it (the GPU box allots a
+    CPU share per GPU and exports OMP_NUM_THREADS for it)."""
+    avail = len(os.sched_getaffinity(0))
+    env = os.environ.get("BENCH_CPU_THREADS") or os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(avail, int(env))) if env else avail
+
+
 def cpu_baseline(x_host, dms, cfg, ntrials, threads):
+    # OpenMP placement must be in the environment before libgomp initialises
+    os.environ.setdefault("OMP_PROC_BIND", "close")
+    os.environ.setdefault("OMP_PLACES", "cores")
     import oracle
     ntrials = min(ntrials, dms.size)
     sel = dms[np.linspace(0, dms.size - 1, ntrials).astype(int)]
@@ -54,19 +87,77 @@ def cpu_baseline(x_host, dms, cfg, ntrials, threads):
     oracle.search(x_host, sel, cfg.start_freq, cfg.bandwidth, cfg.tsamp, nthreads=threads)
     dt = time.perf_counter() - t0
     return {"value": ntrials * cfg.nsamples / dt, "unit": "DM-trial samples/s", "cores": threads,
-            "kind": "port",
+            "kind": "port", "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+            "omp": {"OMP_PROC_BIND": os.environ.get("OMP_PROC_BIND"), "OMP_PLACES": os.environ.get("OMP_PLACES")},
             "sample": f"{ntrials} of the {dms.size} {cfg.name} trials (evenly spaced), full "
-                      f"{cfg.nchan}x2^{int(np.log2(cfg.nsamples))} {cfg.dtype} filterbank, float64 oracle/dedisp_oracle.c (numba prange -> OpenMP), {dt:.1f} s"}
+                      f"{cfg.nchan}x2^{int(np.log2(cfg.nsamples))} {cfg.dtype} filterbank, float64 "
+                      f"oracle/dedisp_oracle.c (numba prange -> OpenMP over trials), {dt:.1f} s"}
 
 
 def load_pmc(workload):
+    """Per-launch HBM bytes of the dominant kernel from the committed PMC summary."""
     path = os.path.join(REPO, "profiles", f"pmc_{workload}.json")
-    if os.path.exists(path):
-        try:
-            return json.load(open(path)).get("hbm_bytes_per_launch")
-        except Exception:
-            return None
-    return None
+    if not os.path.exists(path):
+        return None
+    try:
+        return json.load(open(path))
+    except (OSError, ValueError):
+        return None
+
+
+def clean_bench(dev, steps):
+    """The C4 cleaning pass (configs[3], clean.py:58-133) on device-resident data: the
+    channel masks and renormalize_data(cut_outliers=True) per input dtype."""
+    from pulsarutils import clean
+    cfg = CONFIGS["C4"]
+    res = {"workload": f"C4: {cfg.nchan} chan x 2^{int(np.log2(cfg.nsamples))} RFI filterbank, "
+                       "get_noisier_channels + measure_channel_variability + "
+                       "renormalize_data(cut_outliers=True)", "steps": steps}
+    for dt in ("f32", "u8"):
+        xd = torch.from_numpy(synth.rfi_filterbank_np(cfg, dtype=dt)).to(dev)
+        b_in = xd.element_size()
+        out = torch.empty(xd.shape, dtype=torch.float64, device=dev)
+
+        def masks():
+            bad = clean.get_noisier_channels(xd)
+            return clean.measure_channel_variability(xd, badchans_mask=bad), bad
+
+        def renorm(bad):
+            return clean.renormalize_device(xd, badchans_mask=bad, cut_outliers=True, out=out)
+
+        var, bad = masks()
+        renorm(bad)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            masks()
+        torch.cuda.synchronize()
+        t_mask = (time.perf_counter() - t0) / steps * 1e3
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            _, bins = renorm(bad)
+        torch.cuda.synchronize()
+        t_ren = (time.perf_counter() - t0) / steps * 1e3
+        n_el = float(cfg.nchan) * cfg.nsamples
+        # algorithmic bytes of renormalize(cut_outliers): the zero-DM column pass, the
+        # per-channel mean of x*f and the apply pass each read x once; the apply pass
+        # writes the float64 plane (1-D vectors and the zeroed columns are negligible)
+        alg = n_el * (3 * b_in + 8)
+        mask_bytes = n_el * 2 * b_in  # channel means + variances: two row passes
+        res[dt] = {"masks_ms": round(t_mask, 4), "renormalize_ms": round(t_ren, 4),
+                   "renormalize_alg_bytes": alg,
+                   "renormalize_GBps": round(alg / t_ren / 1e6, 1),
+                   "renormalize_hbm_frac": round(alg / t_ren / 1e6 / HBM_PEAK_GBS, 4),
+                   "masks_alg_bytes": mask_bytes,
+                   "masks_hbm_frac": round(mask_bytes / t_mask / 1e6 / HBM_PEAK_GBS, 4),
+                   "bad_channels": int(bad.sum()), "variable_channels": int(var.sum()),
+                   "bad_bins": int(np.count_nonzero(bins))}
+        del xd, out
+        torch.cuda.empty_cache()
+    res["roofline"] = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "achieved": res["f32"]["renormalize_GBps"], "frac": res["f32"]["renormalize_hbm_frac"],
+                       "what": "f32 renormalize_data(cut_outliers=True) end to end (host steps included)"}
+    return res
 
 
 def main():
@@ -76,8 +167,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--acc", default="native", choices=["native", "f32", "f64"])
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-trials", type=int, default=400)
+    ap.add_argument("--no-clean", action="store_true")
+    ap.add_argument("--clean-steps", type=int, default=5)
+    ap.add_argument("--bcast-chunks", type=int, default=8)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -92,14 +187,20 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
     cfg = CONFIGS[args.config]
-    per_rank = cfg.ntrials
-    # weak scaling: extend the plan to world * ntrials trials, 1-sample steps
-    perdm = 4149.0 * (cfg.start_freq ** -2 - (cfg.start_freq + cfg.bandwidth) ** -2) / cfg.tsamp
-    min_n = cfg.dmmin * perdm
-    dmmax = (min_n + world * per_rank - 1.5) / perdm
-    dms_all = dedispersion_plan(cfg.nchan, cfg.dmmin, dmmax, cfg.start_freq, cfg.bandwidth, cfg.tsamp)
-    assert dms_all.size == world * per_rank, dms_all.size
-    dms = dms_all[rank * per_rank:(rank + 1) * per_rank]
+    if args.scaling == "weak":
+        # extend the plan to world * ntrials trials (1-sample steps, dedispersion.py:149-171)
+        perdm = 4149.0 * (cfg.start_freq ** -2 - (cfg.start_freq + cfg.bandwidth) ** -2) / cfg.tsamp
+        min_n = cfg.dmmin * perdm
+        dmmax = (min_n + world * cfg.ntrials - 1.5) / perdm
+        dms_all = dedispersion_plan(cfg.nchan, cfg.dmmin, dmmax, cfg.start_freq, cfg.bandwidth, cfg.tsamp)
+        if dms_all.size != world * cfg.ntrials:
+            raise RuntimeError(f"weak-scaling grid has {dms_all.size} trials, expected {world * cfg.ntrials}")
+    else:
+        dms_all = dedispersion_plan(cfg.nchan, cfg.dmmin, cfg.dmmax, cfg.start_freq, cfg.bandwidth, cfg.tsamp)
+    lo, hi = shard_bounds(dms_all.size, world, rank)
+    dms = dms_all[lo:hi]
+    per_rank = dms.size
+    chunk = -(-dms_all.size // world)  # equal gather slots
 
     # ---- input: generated on rank 0 in HBM, RCCL-broadcast to the others
     t0 = time.perf_counter()
@@ -110,14 +211,6 @@ def main():
                                                           "f64": torch.float64}[cfg.dtype], device=dev)
     torch.cuda.synchronize()
     log(f"rank {rank}: input ready {time.perf_counter() - t0:.1f}s")
-    bcast_ms = None
-    if world > 1:
-        dist.barrier()
-        torch.cuda.synchronize()
-        tb = time.perf_counter()
-        dist.broadcast(x, src=0)
-        torch.cuda.synchronize()
-        bcast_ms = (time.perf_counter() - tb) * 1e3
 
     acc = {"native": _hip.PU_ACC_NATIVE, "f32": _hip.PU_ACC_F32, "f64": _hip.PU_ACC_F64}[args.acc]
     sh = _hip.shift_table(cfg.nchan, dms, cfg.start_freq, cfg.bandwidth, cfg.tsamp)
@@ -128,13 +221,37 @@ def main():
             torch.empty(per_rank, dtype=torch.float64, device=dev),
             torch.empty(per_rank, dtype=torch.float64, device=dev),
             torch.empty(per_rank, dtype=torch.int32, device=dev))
-    gathered = [torch.empty(world * per_rank, dtype=torch.float64, device=dev) for _ in range(3)]
+    local_stats = torch.zeros((3, chunk), dtype=torch.float64, device=dev)
+    gathered = torch.empty((world, 3, chunk), dtype=torch.float64, device=dev)
+
+    bcast = None
+    if world > 1:
+        from pulsarutils.parallel import pipelined_broadcast_search
+        # broadcast alone (plain RCCL broadcast of the whole filterbank), then the
+        # chunked broadcast with the search of early time chunks overlapping it
+        dist.barrier()
+        torch.cuda.synchronize()
+        tb = time.perf_counter()
+        dist.broadcast(x, src=0)
+        torch.cuda.synchronize()
+        bcast_ms = (time.perf_counter() - tb) * 1e3
+        dist.barrier()
+        torch.cuda.synchronize()
+        tb = time.perf_counter()
+        pipelined_broadcast_search(x, plan, outs, ws, src=0, chunks=args.bcast_chunks)
+        torch.cuda.synchronize()
+        e2e = torch.tensor([(time.perf_counter() - tb) * 1e3], dtype=torch.float64, device=dev)
+        dist.all_reduce(e2e, op=dist.ReduceOp.MAX)
+        bcast = {"broadcast_ms": bcast_ms, "broadcast_GBps": x.numel() * x.element_size() / bcast_ms / 1e6,
+                 "end_to_end_ms": float(e2e.item()), "bcast_chunks": args.bcast_chunks,
+                 "what": "end_to_end_ms: chunked RCCL broadcast of the filterbank + the search of one step, "
+                         "the search of each time chunk launched as soon as its rows (and halo) landed"}
 
     def step():
         plan.search(x, out=outs, workspace=ws)
         if world > 1:
-            for g, o in zip(gathered, outs[:3]):
-                dist.all_gather_into_tensor(g, o)
+            local_stats[:, :per_rank].copy_(torch.stack(outs[:3]))
+            dist.all_gather_into_tensor(gathered, local_stats)
 
     for i in range(args.warmup):
         step()
@@ -157,11 +274,16 @@ def main():
         elapsed = float(tt.item())
     ms_per_step = elapsed / args.steps * 1e3
 
-    # parity spot check on rank 0's best trial (pulse DM)
-    snr = outs[2].cpu().numpy()
-    best_dm = float(dms[np.argmax(snr)])
+    # spot check: best trial of the whole grid (rank 0's view of the gathered S/N)
+    if world > 1:
+        snr_all = np.concatenate([gathered[r, 2, :shard_bounds(dms_all.size, world, r)[1]
+                                           - shard_bounds(dms_all.size, world, r)[0]].cpu().numpy()
+                                  for r in range(world)])
+    else:
+        snr_all = outs[2].cpu().numpy()
+    best_dm = float(dms_all[np.argmax(snr_all)])
 
-    total_samples = world * per_rank * cfg.nsamples
+    total_samples = dms_all.size * cfg.nsamples
     value = total_samples / (ms_per_step / 1e3)
     kernel_ms = float(np.mean(kms)) if len(kms) else None
     adds = float(cfg.nchan) * cfg.nsamples * per_rank
@@ -170,17 +292,26 @@ def main():
     roof = None
     if kernel_ms:
         info = plan.info
+        acc64 = bool(info["acc_is_f64"])
+        peak = VALU_F64_ADD_PEAK_TFLOPS if acc64 else VALU_ADD_PEAK_TFLOPS
         achieved = adds / (kernel_ms / 1e3) / 1e12
-        roof = {"bound": "valu", "achieved": round(achieved, 3), "peak": VALU_ADD_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / VALU_ADD_PEAK_TFLOPS, 4),
-                "traffic": load_pmc(args.config),
+        pmc = load_pmc(args.config) if world == 1 or args.scaling == "weak" else None
+        traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+        roof = {"bound": "valu", "achieved": round(achieved, 3), "peak": peak,
+                "unit": "TFLOP/s" + (" (f64 adds)" if acc64 else " (f32 adds)"),
+                "frac": round(achieved / peak, 4), "traffic": traffic,
                 "kernel": "dedisp_sub_kernel" if info["group"] > 1 else "dedisp_kernel",
                 "kernel_ms": round(kernel_ms, 4),
                 "algorithmic_flop_per_launch": adds, "algorithmic_bytes_per_launch": alg_bytes,
                 "hbm_compulsory_gbs": round(alg_bytes / (kernel_ms / 1e3) / 1e9, 1),
                 "hbm_compulsory_frac": round(alg_bytes / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+        if traffic:
+            roof.update({"hbm_counter_GBps": round(traffic / (kernel_ms / 1e3) / 1e9, 1),
+                         "hbm_counter_frac": round(traffic / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "traffic_source": pmc.get("source"), "traffic_kernel_ms_at_collection":
+                             pmc.get("kernel_ms")})
         if info["group"] > 1:
-            # executed work of the exact subband decomposition (DESIGN.md §4.2): G x fewer
+            # executed work of the exact subband decomposition (DESIGN.md §4.1): G x fewer
             # adds than the algorithm's; the LDS array (256 B/clk/CU) is its binding unit
             lds = info["lds_traffic"] / (kernel_ms / 1e3) / 1e12
             roof.update({"executed_flop_per_launch": info["exec_adds"],
@@ -189,32 +320,38 @@ def main():
                          "lds_peak_TBps": LDS_PEAK_TBPS, "lds_frac": round(lds / LDS_PEAK_TBPS, 4),
                          "group": info["group"]})
 
+    clean = None
+    if rank == 0 and world == 1 and not args.no_clean:
+        log("clean (C4) ...")
+        clean = clean_bench(dev, args.clean_steps)
+        log(f"clean {clean['f32']['renormalize_ms']:.3f} ms f32, {clean['u8']['renormalize_ms']:.3f} ms u8")
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline ...")
         xh = x.cpu().numpy()
-        import oracle
-        threads = int(os.environ.get("BENCH_CPU_THREADS", min(16, os.cpu_count() or 1)))
+        threads = cpu_threads()
         cpu = cpu_baseline(xh, dms, cfg, args.cpu_trials, threads)
         del xh
-        log(f"cpu baseline {cpu['value']:.3e} samples/s on {threads} threads")
+        log(f"cpu baseline {cpu['value']:.3e} samples/s on {threads} threads ({cpu['cpu_model']})")
 
     if rank == 0:
         line = {"metric": "dedispersed DM-trial samples/sec (whole node)", "value": value,
                 "unit": "DM-trial samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": args.scaling,
+                "vs_baseline": None,
                 "dtype": {"f32": "f32", "u8": "u8", "f64": "f64"}[cfg.dtype] + ("" if args.acc == "native"
                                                                                  else f"(acc {args.acc})"),
-                "data": "synthetic (|N(0,0.5)| + unit pulse at DM %g, generated in HBM)" % cfg.pulse_dm,
+                "data": "synthetic (noise + unit pulse at DM %g, generated in HBM)" % cfg.pulse_dm,
                 "config": {"workload": f"{cfg.name}: {cfg.nchan} chan x 2^{int(np.log2(cfg.nsamples))} "
-                                      f"{cfg.dtype} samples, {per_rank} DM trials per GPU",
+                                      f"{cfg.dtype} samples, {dms_all.size} DM trials "
+                                      f"({'per GPU' if args.scaling == 'weak' else 'in all'})",
                            "nchan": cfg.nchan, "nsamples": cfg.nsamples, "trials_per_gpu": per_rank,
-                           "total_trials": world * per_rank, "parallelism": f"dm-shard{world}",
-                           "best_dm_rank0": best_dm},
-                "roofline": roof, "cpu_baseline": cpu}
-        if bcast_ms is not None:
-            line["broadcast_ms"] = bcast_ms
-            line["broadcast_GBps"] = x.numel() * x.element_size() / bcast_ms / 1e6
+                           "total_trials": int(dms_all.size), "parallelism": f"dm-shard{world}",
+                           "best_dm": best_dm},
+                "roofline": roof, "clean": clean, "cpu_baseline": cpu}
+        if bcast is not None:
+            line["multi_gpu"] = bcast
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -89,6 +89,18 @@ int pu_plan_search(pu_plan *plan, const void *data, int64_t ld, double *max_out,
                    double *std_out, double *snr_out, int32_t *rebin_out, void *workspace,
                    size_t workspace_bytes, void *stream);
 
+/* pu_plan_search split in two, for pipelining (multi-GPU: the search of early time
+ * chunks overlaps the broadcast of later ones).  search_tiles runs the
+ * shift-and-sum + per-tile statistics of time tiles [tt_begin, tt_end) only (time
+ * tile = pu_plan_info "time_tile" samples; a tile reads its window plus the shift
+ * halo, modulo nsamples); once every tile has run, finalize combines the per-tile
+ * records into the per-trial outputs exactly as pu_plan_search does. */
+int pu_plan_search_tiles(pu_plan *plan, const void *data, int64_t ld, int64_t tt_begin,
+                         int64_t tt_end, void *workspace, size_t workspace_bytes, void *stream);
+int pu_plan_finalize(pu_plan *plan, double *max_out, double *std_out, double *snr_out,
+                     int32_t *rebin_out, const void *workspace, size_t workspace_bytes,
+                     void *stream);
+
 /* Replaces dedisperse (dedispersion.py:93-98) for every trial of the plan: writes
  * the dedispersed plane plane[trial * ld_plane + t] in the accumulation type
  * (float32 or float64), the show=True plane of dedispersion_search (:214-227). */
@@ -157,6 +169,18 @@ int pu_ratio_dev(const double *numerator, const double *x, int64_t n, double *ou
 int pu_renorm_apply(const void *x, int dtype, int64_t nchan, int64_t n, int64_t ld,
                     const double *factor, const double *spec, const uint8_t *bad,
                     double *out, int64_t ld_out, double *col_means, void *stream);
+
+/* Opt-in zero-DM subtraction (BASELINE north_star "zero-DM subtraction"; the reference
+ * has no counterpart: clean.py:77-82 only DIVIDES by the smoothed zero-DM series, so
+ * renormalize_data keeps this off by default).  As pu_renorm_apply, then for every
+ * good channel out[c][t] -= S[t] / ngood, S[t] = the in-order sum over channels of the
+ * normalised values (bad channels contribute +0.0); bad channels stay 0.  ngood =
+ * the number of channels with bad[c] == 0.  col_means (if not NULL) is S[t] / nchan,
+ * i.e. the cut_outliers light curve of the data BEFORE the subtraction. */
+int pu_renorm_apply_zero_dm(const void *x, int dtype, int64_t nchan, int64_t n, int64_t ld,
+                            const double *factor, const double *spec, const uint8_t *bad,
+                            int64_t ngood, double *out, int64_t ld_out, double *col_means,
+                            void *stream);
 
 /* out[:, cols[k]] = 0 for k < ncols (clean.py:105). cols: device int64. */
 int pu_zero_columns(double *out, int64_t nrows, int64_t ld_out, const int64_t *cols,

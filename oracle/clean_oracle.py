@@ -51,12 +51,17 @@ def channel_variability(array, badchans_mask=None):
 
 
 def renormalize(array, badchans_mask=None, baseline_window=101, cut_outliers=False,
-                return_badbins=False):
+                return_badbins=False, zero_dm=False):
     """clean.py:70-111.
 
     float64 copy; zero-DM series over good channels; gaussian-smoothed
     multiplicative normalisation; per-channel (x - mu)/mu; bad channels zeroed;
     optional zero-DM time-bin cut where only the last window (16) survives.
+
+    ``zero_dm`` (NOT in the reference - parity unpinned, restated from the build's
+    documented contract, include/pulsarutils_hip.h pu_renorm_apply_zero_dm): subtract
+    S[t]/ngood from the good channels, S = the in-order sum over channels of the
+    normalised data; the outlier cut then uses S/nchan (the pre-subtraction mean).
     """
     x = np.asarray(array).astype(float)
     nchan = x.shape[0]
@@ -71,9 +76,16 @@ def renormalize(array, badchans_mask=None, baseline_window=101, cut_outliers=Fal
     x -= spec[:, None]
     x /= spec[:, None]
     x[badchans_mask, :] = 0
+    lc_pre = None
+    if zero_dm:
+        s = x.sum(0)
+        lc_pre = s / nchan
+        ngood = nchan - int(np.count_nonzero(badchans_mask))
+        if ngood:
+            x[~badchans_mask, :] -= (s / ngood)[None, :]
     bad_bins = None
     if cut_outliers:
-        lc = x.mean(0)
+        lc = x.mean(0) if lc_pre is None else lc_pre
         window = 16
         lc_rebin = uniform_filter1d(lc, window)
         sd = np.std(lc_rebin[::window])

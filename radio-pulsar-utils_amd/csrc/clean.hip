@@ -349,31 +349,61 @@ __global__ void ratio_kernel(double num, const double *__restrict__ x, int64_t n
 // (x*f - mu)/mu per element, bad channels written as 0.0, column mean of the result
 // accumulated over channels in order.  Same column layout as colmean_kernel; the
 // channel means and bad flags are staged in LDS per row chunk.
-template <typename Tin, int V, bool NT>
+//
+// ZDM (opt-in zero-DM subtraction, no reference counterpart: clean.py:77-82 only
+// divides by the smoothed zero-DM series): the strip is walked twice.  The first walk
+// sums the normalised values over channels in order (bad channels add +0.0, so the sum
+// is the good channels' sum bit for bit); the second writes e - S[t]/ngood for good
+// channels and 0.0 for bad ones.  col_means (the cut_outliers series) is S[t]/nchan of
+// the normalised data BEFORE the subtraction, as without ZDM.
+template <typename Tin, int V, bool NT, bool ZDM>
 __global__ void __launch_bounds__(256)
 apply_kernel(const Tin *__restrict__ x, int64_t nchan, int64_t col0, int64_t ncols, int64_t ld,
              const double *__restrict__ factor, const double *__restrict__ spec,
              const uint8_t *__restrict__ bad, double *__restrict__ out, int64_t ld_out,
-             double *__restrict__ col_means)
+             double *__restrict__ col_means, int64_t ngood)
 {
     __shared__ double mus[kRowChunk];
     __shared__ uint8_t bads[kRowChunk];
     const int64_t c = col0 + ((int64_t)blockIdx.x * 256 + threadIdx.x) * V;
     const bool active = c < col0 + ncols;
-    double f[V], acc[V];
+    double f[V], acc[V], zsub[V];
 #pragma unroll
     for (int j = 0; j < V; ++j) {
         f[j] = active ? factor[c + j] : 0.0;
         acc[j] = 0.0;
+        zsub[j] = 0.0;
     }
-    for (int64_t r0 = 0; r0 < nchan; r0 += kRowChunk) {
-        const int rn = (int)(nchan - r0 < kRowChunk ? nchan - r0 : kRowChunk);
+    auto stage = [&](int64_t r0, int rn) {
         __syncthreads();
         for (int i = threadIdx.x; i < rn; i += 256) {
             mus[i] = spec[r0 + i];
             bads[i] = bad ? bad[r0 + i] : 0;
         }
         __syncthreads();
+    };
+    if constexpr (ZDM) {
+        for (int64_t r0 = 0; r0 < nchan; r0 += kRowChunk) {
+            const int rn = (int)(nchan - r0 < kRowChunk ? nchan - r0 : kRowChunk);
+            stage(r0, rn);
+            if (!active) continue;
+            walk_rows<Tin, V>(x + r0 * ld + c, ld, rn, [&](int i, const Vec<Tin, V> &v) {
+                const double mu = mus[i];
+                const bool b = bads[i] != 0;
+#pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    double e = static_cast<double>(v.v[j]) * f[j];
+                    e = (e - mu) / mu;
+                    acc[j] += b ? 0.0 : e;
+                }
+            });
+        }
+#pragma unroll
+        for (int j = 0; j < V; ++j) zsub[j] = ngood > 0 ? acc[j] / static_cast<double>(ngood) : 0.0;
+    }
+    for (int64_t r0 = 0; r0 < nchan; r0 += kRowChunk) {
+        const int rn = (int)(nchan - r0 < kRowChunk ? nchan - r0 : kRowChunk);
+        stage(r0, rn);
         if (!active) continue;
         double *o = out + r0 * ld_out + c;
         walk_rows<Tin, V>(x + r0 * ld + c, ld, rn, [&](int i, const Vec<Tin, V> &v) {
@@ -384,8 +414,12 @@ apply_kernel(const Tin *__restrict__ x, int64_t nchan, int64_t col0, int64_t nco
             for (int j = 0; j < V; ++j) {
                 double e = static_cast<double>(v.v[j]) * f[j];
                 e = (e - mu) / mu;
-                res.v[j] = b ? 0.0 : e;
-                acc[j] += res.v[j];
+                if constexpr (ZDM) {
+                    res.v[j] = b ? 0.0 : e - zsub[j];
+                } else {
+                    res.v[j] = b ? 0.0 : e;
+                    acc[j] += res.v[j];
+                }
             }
             if constexpr (NT) {
 #pragma unroll
@@ -666,20 +700,24 @@ bool nt_stores(size_t elem)
 
 template <typename Tin>
 int renorm_apply_t(const void *x, int64_t nchan, int64_t n, int64_t ld, const double *factor, const double *spec,
-                   const uint8_t *bad, double *out, int64_t ld_out, double *col_means, hipStream_t s)
+                   const uint8_t *bad, double *out, int64_t ld_out, double *col_means, int64_t ngood_zdm,
+                   hipStream_t s)
 {
     const int vm = vec_max(sizeof(Tin), 1);
     const int v = std::min(pick_vec<Tin>(x, ld, vm), pick_vec<double>(out, ld_out, vm));
+    const bool zdm = ngood_zdm >= 0;
     return column_launches<Tin>(v, n, [&](auto vc, int64_t col0, int64_t ncols) {
         constexpr int V = decltype(vc)::value;
-        if (nt_stores(sizeof(Tin)))
-            hipLaunchKernelGGL((apply_kernel<Tin, V, true>), dim3(blocks_for(ncols / V, 256)), dim3(256), 0, s,
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(blocks_for(ncols / V, 256)), dim3(256), 0, s,
                                reinterpret_cast<const Tin *>(x), nchan, col0, ncols, ld, factor, spec, bad, out,
-                               ld_out, col_means);
+                               ld_out, col_means, ngood_zdm);
+        };
+        const bool nt = nt_stores(sizeof(Tin));
+        if (zdm)
+            nt ? go(apply_kernel<Tin, V, true, true>) : go(apply_kernel<Tin, V, false, true>);
         else
-            hipLaunchKernelGGL((apply_kernel<Tin, V, false>), dim3(blocks_for(ncols / V, 256)), dim3(256), 0, s,
-                               reinterpret_cast<const Tin *>(x), nchan, col0, ncols, ld, factor, spec, bad, out,
-                               ld_out, col_means);
+            nt ? go(apply_kernel<Tin, V, true, false>) : go(apply_kernel<Tin, V, false, false>);
     });
 }
 
@@ -747,20 +785,37 @@ int pu_ratio(double num, const double *x, int64_t n, double *out, void *stream)
     return pu::launch_check("ratio_kernel");
 }
 
-int pu_renorm_apply(const void *x, int dtype, int64_t nchan, int64_t n, int64_t ld, const double *factor,
-                    const double *spec, const uint8_t *bad, double *out, int64_t ld_out, double *col_means,
-                    void *stream)
+static int renorm_apply_any(const void *x, int dtype, int64_t nchan, int64_t n, int64_t ld, const double *factor,
+                            const double *spec, const uint8_t *bad, double *out, int64_t ld_out, double *col_means,
+                            int64_t ngood_zdm, void *stream)
 {
     PU_REQUIRE(x && factor && spec && out, "pu_renorm_apply: NULL pointer");
     PU_REQUIRE(nchan > 0 && n > 0 && ld >= n && ld_out >= n, "pu_renorm_apply: bad shape");
     hipStream_t s = pu::as_stream(stream);
+    const int64_t g = ngood_zdm;
     switch (dtype) {
-    case PU_U8: renorm_apply_t<uint8_t>(x, nchan, n, ld, factor, spec, bad, out, ld_out, col_means, s); break;
-    case PU_F32: renorm_apply_t<float>(x, nchan, n, ld, factor, spec, bad, out, ld_out, col_means, s); break;
-    case PU_F64: renorm_apply_t<double>(x, nchan, n, ld, factor, spec, bad, out, ld_out, col_means, s); break;
+    case PU_U8: renorm_apply_t<uint8_t>(x, nchan, n, ld, factor, spec, bad, out, ld_out, col_means, g, s); break;
+    case PU_F32: renorm_apply_t<float>(x, nchan, n, ld, factor, spec, bad, out, ld_out, col_means, g, s); break;
+    case PU_F64: renorm_apply_t<double>(x, nchan, n, ld, factor, spec, bad, out, ld_out, col_means, g, s); break;
     default: pu::set_error("pu_renorm_apply: unsupported dtype %d", dtype); return PU_EUNSUPPORTED;
     }
     return pu::launch_check("apply_kernel");
+}
+
+int pu_renorm_apply(const void *x, int dtype, int64_t nchan, int64_t n, int64_t ld, const double *factor,
+                    const double *spec, const uint8_t *bad, double *out, int64_t ld_out, double *col_means,
+                    void *stream)
+{
+    return renorm_apply_any(x, dtype, nchan, n, ld, factor, spec, bad, out, ld_out, col_means, -1, stream);
+}
+
+int pu_renorm_apply_zero_dm(const void *x, int dtype, int64_t nchan, int64_t n, int64_t ld, const double *factor,
+                            const double *spec, const uint8_t *bad, int64_t ngood, double *out, int64_t ld_out,
+                            double *col_means, void *stream)
+{
+    PU_REQUIRE(ngood >= 0 && ngood <= nchan, "pu_renorm_apply_zero_dm: ngood %lld outside [0, nchan]",
+               (long long)ngood);
+    return renorm_apply_any(x, dtype, nchan, n, ld, factor, spec, bad, out, ld_out, col_means, ngood, stream);
 }
 
 size_t pu_median_workspace_bytes(void) { return sizeof(MedState) + 2 * kMedBins * sizeof(uint32_t); }

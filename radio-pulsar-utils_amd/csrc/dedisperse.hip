@@ -59,7 +59,9 @@ struct DedispArgs {
     int32_t ncc;
     int32_t row_stride;
     int32_t small_n;
-    int32_t pad0;
+    int32_t tt0;      // first time tile of this launch (time-tile range launches)
+    int32_t ntt_run;  // time tiles this launch covers (grid = ndt x ntt_run)
+    int32_t pad1;
     void *plane;
     int64_t ld_plane;
     double *partials;
@@ -351,7 +353,7 @@ dedisp_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const int32_
 
     const int wg = pu::xcd_remap(blockIdx.x, gridDim.x);
     const int dt = wg % a.ndt;
-    const int tt = wg / a.ndt;
+    const int tt = a.tt0 + wg / a.ndt;
     const int t0 = tt * TT;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -719,7 +721,7 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
     const int ndt = o.ndt;
     const int wg = pu::xcd_remap(blockIdx.x, gridDim.x);
     const int dt = wg % ndt;
-    const int tt = wg / ndt;
+    const int tt = o.tt0 + wg / ndt;
     const int t0 = tt * TT;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -990,9 +992,18 @@ int pick_variant(int dtype, int acc)
     }
 }
 
+// Host-side subband tables of a candidate plan (uploaded only for the plan that is kept).
+struct SubHost {
+    std::vector<i32x4> tiles, stages;
+    std::vector<i32x2> tile_stages;
+    std::vector<int32_t> slots, base;
+    std::vector<uint32_t> recs;
+};
+
 }  // namespace
 
 struct pu_plan {
+    SubHost host;
     int dtype = 0, acc = 0, variant = 0;
     int64_t nchan = 0, n = 0, ndm = 0;
     int K = 0, TT = 0;
@@ -1031,7 +1042,7 @@ int ensure_lds(Kern kern, size_t bytes)
 template <typename Tin, typename Tl, typename Ta>
 int launch_variant(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
 {
-    const dim3 grid((unsigned)((int64_t)p->ndt * p->ntt)), block(kThreads);
+    const dim3 grid((unsigned)((int64_t)p->ndt * a.ntt_run)), block(kThreads);
     if (plane) {
         auto kern = dedisp_kernel<Tin, Tl, Ta, true, false>;
         int rc = ensure_lds(kern, p->lds_bytes);
@@ -1072,7 +1083,7 @@ int launch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
     sa.zero_len = (int32_t)p->zero_len;
     sa.lds_bytes = (int32_t)p->lds_bytes;
     if (const char *env = getenv("PU_SUB_SKIP")) sa.skip = atoi(env);
-    const dim3 grid((unsigned)((int64_t)p->ndt * p->ntt)), block(C::THREADS);
+    const dim3 grid((unsigned)((int64_t)p->ndt * a.ntt_run)), block(C::THREADS);
     auto go = [&](auto kern) {
         int rc = ensure_lds(kern, p->lds_bytes);
         if (rc) return rc;
@@ -1574,13 +1585,29 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     p->nstages = (int64_t)stages.size();
     p->exec_adds = adds_tile * ntt;
     p->lds_traffic = lds_tile * ntt;
+    // host tables only: the caller uploads the plan it keeps (upload_sub), so comparing
+    // candidate group sizes costs no device memory
+    SubHost &h = p->host;
+    h.tiles = std::move(tiles);
+    h.tile_stages = std::move(tile_stages);
+    h.stages = std::move(stages);
+    h.slots = std::move(slotmeta);
+    h.recs = std::move(rec);
+    h.base = dma ? std::move(base) : std::vector<int32_t>();
+    return PU_OK;
+}
+
+int upload_sub(pu_plan *p)
+{
+    SubHost &h = p->host;
     int rc = PU_OK;
-    if (!rc) rc = upload(&p->d_tiles, tiles);
-    if (!rc) rc = upload(&p->d_tile_stages, tile_stages);
-    if (!rc) rc = upload(&p->d_stages, stages);
-    if (!rc) rc = upload(&p->d_slots, slotmeta);
-    if (!rc) rc = upload(&p->d_recs, rec);
-    if (!rc && dma) rc = upload(&p->d_base, base);
+    if (!rc) rc = upload(&p->d_tiles, h.tiles);
+    if (!rc) rc = upload(&p->d_tile_stages, h.tile_stages);
+    if (!rc) rc = upload(&p->d_stages, h.stages);
+    if (!rc) rc = upload(&p->d_slots, h.slots);
+    if (!rc) rc = upload(&p->d_recs, h.recs);
+    if (!rc && !h.base.empty()) rc = upload(&p->d_base, h.base);
+    h = SubHost{};
     return rc;
 }
 
@@ -1662,14 +1689,19 @@ int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int
     G = std::min(G, 8);
     if (kVariants[v].acc_f64) G = 1;
     while (G > 1 && G >= nchan) G >>= 1;
+    // The automatic choice is calibrated on the wide shape with DMA-staged rows (f32, or
+    // u8 with n % 4 == 0); elsewhere the default stays G = 4.
+    const bool dma_rows = dtype == PU_F32 || (dtype == PU_U8 && n % 4 == 0);
+    if (auto_g && (shape != SUB_WIDE || !dma_rows || getenv("PU_LDS_BUDGET_KB"))) auto_g = false;
     int rc = PU_EUNSUPPORTED;
     if (auto_g) {
-        // Default group size: plan G = 8 and G = 4 and keep the cheaper by the measured
-        // cost model: LDS bytes + 3.0e6 B-equivalent per (stage, time tile).
-        // G = 8 halves the LDS traffic at C3 (1240 vs 1328 ms) but its extra stages cost
-        // more than that at C2 (22.7 vs 18.4 ms) and C5.
+        // Default group size: plan G = 8 and G = 4 on the host and keep the cheaper by the
+        // measured cost model: LDS bytes + 3.0e6 B-equivalent per (stage,
+        // time tile).  G = 8 halves the LDS traffic at C3 (1240 vs 1328 ms) but its extra
+        // stages cost more than that at C2 (22.7 vs 18.4 ms) and C5.  Only the winner's
+        // tables are uploaded.  A candidate that does not fit (PU_EUNSUPPORTED) is not
+        // viable; any other error is returned as is.
         auto cost = [](const pu_plan *q) { return (double)q->lds_traffic + 3.0e6 * (double)q->nstages * q->ntt; };
-        // both candidates are built once (the G = 8 one in a second plan object)
         pu_plan *q = new pu_plan();
         q->dtype = p->dtype;
         q->acc = p->acc;
@@ -1680,23 +1712,39 @@ int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int
         q->K = p->K;
         q->TT = p->TT;
         q->ntt = p->ntt;
-        const bool ok8 = plan_sub(q, shifts, 8, shape, sub_budget) == PU_OK;
-        const bool ok4 = plan_sub(p, shifts, 4, shape, sub_budget) == PU_OK;
-        if (ok8 && (!ok4 || cost(p) > cost(q))) {
+        const int rc8 = plan_sub(q, shifts, 8, shape, sub_budget);
+        const int rc4 = plan_sub(p, shifts, 4, shape, sub_budget);
+        for (int r : {rc8, rc4}) {
+            if (r != PU_OK && r != PU_EUNSUPPORTED) {
+                free_plan(q);
+                free_plan(p);
+                return r;
+            }
+        }
+        pu_plan *keep = nullptr;
+        if (rc8 == PU_OK && (rc4 != PU_OK || cost(p) > cost(q))) {
             free_plan(p);
-            *out = q;
+            keep = q;
+        } else if (rc4 == PU_OK) {
+            free_plan(q);
+            keep = p;
+        }
+        if (keep) {
+            rc = upload_sub(keep);
+            if (rc) {
+                free_plan(keep);
+                return rc;
+            }
+            *out = keep;
             return PU_OK;
         }
         free_plan(q);
-        if (ok4) {
-            *out = p;
-            return PU_OK;
-        }
         reset_tables(p);
-        rc = PU_EUNSUPPORTED;
+        G = 2;  // 8 and 4 do not fit: continue with the smaller groups
     }
     for (; G > 1 && rc == PU_EUNSUPPORTED; G >>= 1) {
         rc = plan_sub(p, shifts, G, shape, sub_budget);
+        if (rc == PU_OK) rc = upload_sub(p);
         if (rc == PU_EUNSUPPORTED) reset_tables(p);
     }
     if (rc == PU_EUNSUPPORTED) rc = plan_channels(p, shifts, budget);
@@ -1776,10 +1824,41 @@ static DedispArgs make_args(const pu_plan *p, const void *data, int64_t ld)
     a.n = (int32_t)p->n;
     a.ndt = p->ndt;
     a.ntt = p->ntt;
+    a.tt0 = 0;
+    a.ntt_run = p->ntt;
     a.ncc = p->ncc;
     a.row_stride = p->row_stride;
     a.small_n = p->small_n;
     return a;
+}
+
+int pu_plan_search_tiles(pu_plan *p, const void *data, int64_t ld, int64_t tt_begin, int64_t tt_end,
+                         void *workspace, size_t ws_bytes, void *stream)
+{
+    int rc = check_data(p, data, ld);
+    if (rc) return rc;
+    PU_REQUIRE(0 <= tt_begin && tt_begin <= tt_end && tt_end <= p->ntt,
+               "pu_plan_search_tiles: tile range [%lld, %lld) outside [0, %d)", (long long)tt_begin,
+               (long long)tt_end, p->ntt);
+    PU_REQUIRE(workspace && ws_bytes >= pu_plan_workspace_bytes(p), "pu_plan_search_tiles: workspace too small");
+    if (tt_begin == tt_end) return PU_OK;
+    DedispArgs a = make_args(p, data, ld);
+    a.partials = reinterpret_cast<double *>(workspace);
+    a.tt0 = (int32_t)tt_begin;
+    a.ntt_run = (int32_t)(tt_end - tt_begin);
+    return dispatch(p, a, false, pu::as_stream(stream));
+}
+
+int pu_plan_finalize(pu_plan *p, double *max_out, double *std_out, double *snr_out, int32_t *rebin_out,
+                     const void *workspace, size_t ws_bytes, void *stream)
+{
+    PU_REQUIRE(p != nullptr, "plan is NULL");
+    PU_REQUIRE(max_out && std_out && snr_out && rebin_out, "pu_plan_finalize: NULL output");
+    PU_REQUIRE(workspace && ws_bytes >= pu_plan_workspace_bytes(p), "pu_plan_finalize: workspace too small");
+    hipLaunchKernelGGL(pu_finalize_kernel, dim3((unsigned)p->ndm), dim3(256), 0, pu::as_stream(stream),
+                       reinterpret_cast<const double *>(workspace), p->ntt, (int)p->n, p->TT, max_out, std_out,
+                       snr_out, rebin_out);
+    return pu::launch_check("pu_finalize_kernel");
 }
 
 int pu_plan_search(pu_plan *p, const void *data, int64_t ld, double *max_out, double *std_out,

@@ -33,6 +33,8 @@ SIGNATURES = {
     "pu_plan_workspace_bytes": (_sz, [_vp]),
     "pu_plan_search": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "pu_plan_dedisperse": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp]),
+    "pu_plan_search_tiles": (_i32, [_vp, _vp, _i64, _i64, _i64, _vp, _sz, _vp]),
+    "pu_plan_finalize": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "pu_plan_info": (_i32, [_vp, _vp, _i32]),
     "pu_plan_enable_timing": (_i32, [_vp, _i32]),
     "pu_plan_kernel_times": (_i32, [_vp, _vp, _i32]),
@@ -45,6 +47,7 @@ SIGNATURES = {
     "pu_median": (_i32, [_vp, _i64, _vp, _vp, _sz, _vp]),
     "pu_ratio_dev": (_i32, [_vp, _vp, _i64, _vp, _vp]),
     "pu_renorm_apply": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
+    "pu_renorm_apply_zero_dm": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp]),
     "pu_zero_columns": (_i32, [_vp, _i64, _i64, _vp, _i64, _vp]),
     "pu_rebin_time": (_i32, [_vp, _i32, _i64, _i64, _i64, _i64, _vp, _vp]),
     "pu_rebin_chan": (_i32, [_vp, _i32, _i64, _i64, _i64, _i64, _vp, _vp]),
@@ -157,8 +160,9 @@ class Plan:
         mode, 2/4/8); float64 accumulation always uses channel mode."""
         require_gpu()
         sh = np.ascontiguousarray(shifts, dtype=np.int64)
+        if sh.ndim != 2 or sh.shape[1] != int(nchan):
+            raise ValueError(f"shift table must be (ndm, {nchan}) int64, got shape {sh.shape}")
         ndm = sh.shape[0]
-        assert sh.shape == (ndm, nchan)
         h = ctypes.c_void_p()
         check(lib().pu_plan_create_grouped(ctypes.byref(h), dtype_code_, acc, nchan, nsamples,
                                            sh.ctypes.data_as(ctypes.c_void_p), ndm, int(group)),
@@ -166,6 +170,10 @@ class Plan:
         self._h = h
         self.dtype_code = dtype_code_
         self.nchan, self.nsamples, self.ndm = nchan, nsamples, ndm
+        # shift extent of the grid: a time tile [t0, t0 + TT) reads samples
+        # [t0 + shift_min, t0 + TT + shift_max] (mod nsamples) of some channel
+        self.shift_min = int(sh.min()) if sh.size else 0
+        self.shift_max = int(sh.max()) if sh.size else 0
         info = np.zeros(len(INFO_FIELDS), np.int64)
         lib().pu_plan_info(h, info.ctypes.data_as(ctypes.c_void_p), len(INFO_FIELDS))
         self.info = dict(zip(INFO_FIELDS, info.tolist()))
@@ -182,9 +190,21 @@ class Plan:
         return bool(self.info["acc_is_f64"])
 
     def _check_data(self, data):
-        assert data.is_cuda and data.dim() == 2 and data.stride(1) == 1
-        assert tuple(data.shape) == (self.nchan, self.nsamples), (tuple(data.shape), self.nchan, self.nsamples)
-        assert dtype_code(data.dtype) == self.dtype_code
+        """Validate before any launch (raises, never asserts: under ``python -O`` an
+        assert would vanish and a wrong-shaped tensor would be read out of bounds)."""
+        t = torch()
+        if not isinstance(data, t.Tensor) or not data.is_cuda:
+            raise ValueError("plan data must be a CUDA (HIP) torch.Tensor")
+        if data.dim() != 2 or data.stride(1) != 1:
+            raise ValueError(f"plan data must be a 2-D row-major tensor, got shape {tuple(data.shape)} "
+                             f"strides {tuple(data.stride())}")
+        if tuple(data.shape) != (self.nchan, self.nsamples):
+            raise ValueError(f"data shape {tuple(data.shape)} does not match the plan "
+                             f"({self.nchan}, {self.nsamples})")
+        if data.stride(0) < self.nsamples:
+            raise ValueError(f"row stride {data.stride(0)} < nsamples {self.nsamples}")
+        if dtype_code(data.dtype) != self.dtype_code:
+            raise ValueError(f"data dtype {data.dtype} does not match the plan's dtype code {self.dtype_code}")
 
     @staticmethod
     def _rows_aligned(data):
@@ -203,12 +223,58 @@ class Plan:
         if out is None:
             out = (t.empty(self.ndm, dtype=t.float64, device=dev), t.empty(self.ndm, dtype=t.float64, device=dev),
                    t.empty(self.ndm, dtype=t.float64, device=dev), t.empty(self.ndm, dtype=t.int32, device=dev))
+        else:
+            want = (t.float64, t.float64, t.float64, t.int32)
+            if len(out) != 4 or any(o.dtype != w or o.numel() < self.ndm or not o.is_contiguous() or o.device != dev
+                                    for o, w in zip(out, want)):
+                raise ValueError(f"out must be 3 float64 + 1 int32 contiguous tensors of >= {self.ndm} "
+                                 f"elements on {dev}")
         if workspace is None:
             workspace = t.empty(max(self.workspace_bytes, 16), dtype=t.uint8, device=dev)
+        elif workspace.device != dev or not workspace.is_contiguous():
+            raise ValueError("workspace must be a contiguous tensor on the data's device")
         check(lib().pu_plan_search(self._h, ptr(data), data.stride(0), ptr(out[0]), ptr(out[1]), ptr(out[2]),
                                    ptr(out[3]), ptr(workspace), workspace.numel(), stream_ptr(stream)),
               "pu_plan_search")
         return out
+
+    def _outs_ws(self, dev, out, workspace):
+        t = torch()
+        if out is None:
+            out = (t.empty(self.ndm, dtype=t.float64, device=dev), t.empty(self.ndm, dtype=t.float64, device=dev),
+                   t.empty(self.ndm, dtype=t.float64, device=dev), t.empty(self.ndm, dtype=t.int32, device=dev))
+        if workspace is None:
+            workspace = t.empty(max(self.workspace_bytes, 16), dtype=t.uint8, device=dev)
+        if workspace.numel() < self.workspace_bytes or workspace.device != dev:
+            raise ValueError(f"workspace must hold {self.workspace_bytes} bytes on {dev}")
+        return out, workspace
+
+    def search_tiles(self, data, tt_begin, tt_end, workspace, stream=None):
+        """Shift-and-sum + per-tile statistics of time tiles [tt_begin, tt_end) only
+        (pu_plan_search_tiles); ``finalize`` after every tile has run."""
+        self._check_data(data)
+        data = self._rows_aligned(data)
+        _, workspace = self._outs_ws(data.device, (), workspace)
+        check(lib().pu_plan_search_tiles(self._h, ptr(data), data.stride(0), int(tt_begin), int(tt_end),
+                                         ptr(workspace), workspace.numel(), stream_ptr(stream)),
+              "pu_plan_search_tiles")
+
+    def finalize(self, workspace, out=None, stream=None):
+        """Per-trial (max, std, snr, rebin) from the per-tile records (pu_plan_finalize)."""
+        out, workspace = self._outs_ws(workspace.device, out, workspace)
+        check(lib().pu_plan_finalize(self._h, ptr(out[0]), ptr(out[1]), ptr(out[2]), ptr(out[3]), ptr(workspace),
+                                     workspace.numel(), stream_ptr(stream)), "pu_plan_finalize")
+        return out
+
+    def tile_window(self, tt):
+        """Half-open sample range [a, b) (NOT reduced mod nsamples) time tile ``tt``
+        may read: a staged row starts at the tile's smallest shift of its channel
+        (rounded down to a dword for 8-bit rows) and spans TT + the tile's largest shift
+        spread + 1 samples, rounded up to whole 256-byte LDS-DMA pieces."""
+        tt_len = self.info["time_tile"]
+        t0 = int(tt) * tt_len
+        return (t0 + self.shift_min - 8,
+                t0 + tt_len + self.shift_max + self.info["max_spread"] + 1 + 256 + 8)
 
     def enable_timing(self, nslots):
         check(lib().pu_plan_enable_timing(self._h, int(nslots)), "pu_plan_enable_timing")
@@ -225,9 +291,12 @@ class Plan:
         t = torch()
         self._check_data(data)
         data = self._rows_aligned(data)
+        pdt = t.float64 if self.acc_is_f64 else t.float32
         if plane is None:
-            plane = t.empty((self.ndm, self.nsamples), dtype=t.float64 if self.acc_is_f64 else t.float32,
-                            device=data.device)
+            plane = t.empty((self.ndm, self.nsamples), dtype=pdt, device=data.device)
+        elif (plane.dtype != pdt or plane.dim() != 2 or plane.shape[0] < self.ndm or plane.shape[1] < self.nsamples
+              or plane.stride(1) != 1 or plane.device != data.device):
+            raise ValueError(f"plane must be a row-major ({self.ndm}, {self.nsamples}) {pdt} tensor on {data.device}")
         check(lib().pu_plan_dedisperse(self._h, ptr(data), data.stride(0), ptr(plane), plane.stride(0),
                                        stream_ptr(stream)), "pu_plan_dedisperse")
         return plane

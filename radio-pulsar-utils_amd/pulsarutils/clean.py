@@ -133,7 +133,8 @@ def _gaussian_weights(sigma):
     return np.ascontiguousarray(_gaussian_kernel1d(sigma, 0, radius)[::-1]), radius
 
 
-def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=False, out=None):
+def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=False, out=None,
+                       zero_dm=False):
     """renormalize_data on a device tensor; returns (float64 device tensor, bad_bins or None).
 
     Passes (clean.py:73-105): zero-DM light curve over good channels (column means,
@@ -142,6 +143,10 @@ def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=
     -> per-channel mean of x*factor (numpy pairwise order) -> (x*f - mu)/mu with bad
     channels zeroed [+ its column mean] -> host uniform_filter1d(16) thresholds ->
     zero the bad time bins.
+
+    ``zero_dm=True`` (opt-in; the reference has no counterpart, see renormalize_data)
+    also subtracts, per time bin, the mean of the normalised good channels, fused into
+    the apply pass (pu_renorm_apply_zero_dm).
     """
     t = _hip.torch()
     nchan, n = x.shape
@@ -169,9 +174,15 @@ def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=
     if out is None:
         out = t.empty((nchan, n), dtype=t.float64, device=dev)
     col = t.empty(n, dtype=t.float64, device=dev) if cut_outliers else None
-    _hip.check(lib.pu_renorm_apply(_hip.ptr(x), code, nchan, n, x.stride(0), _hip.ptr(factor), _hip.ptr(spec),
-                                   _hip.ptr(bad), _hip.ptr(out), out.stride(0), _hip.ptr(col), s),
-               "pu_renorm_apply")
+    if zero_dm:
+        ngood = int(nchan - np.count_nonzero(bad_np))
+        _hip.check(lib.pu_renorm_apply_zero_dm(_hip.ptr(x), code, nchan, n, x.stride(0), _hip.ptr(factor),
+                                               _hip.ptr(spec), _hip.ptr(bad), ngood, _hip.ptr(out), out.stride(0),
+                                               _hip.ptr(col), s), "pu_renorm_apply_zero_dm")
+    else:
+        _hip.check(lib.pu_renorm_apply(_hip.ptr(x), code, nchan, n, x.stride(0), _hip.ptr(factor), _hip.ptr(spec),
+                                       _hip.ptr(bad), _hip.ptr(out), out.stride(0), _hip.ptr(col), s),
+                   "pu_renorm_apply")
     bad_bins = None
     if cut_outliers:
         lc2 = _host(col)
@@ -189,11 +200,20 @@ def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=
 
 
 def renormalize_data(array, diagnostic_figure=None, badchans_mask=None, baseline_window=101,
-                     cut_outliers=False):
-    """clean.py:70-111: zero-DM normalisation + per-channel (x - mu)/mu, float64 out."""
+                     cut_outliers=False, zero_dm=False):
+    """clean.py:70-111: zero-DM normalisation + per-channel (x - mu)/mu, float64 out.
+
+    ``zero_dm`` (default False, so the drop-in is the reference bit for bit): also
+    subtract the zero-DM series - per time bin, the mean over good channels of the
+    normalised data - from every good channel.  The reference only divides by the
+    smoothed zero-DM series (clean.py:77-82); this opt-in subtraction is the
+    north-star cleaning step and has no reference counterpart (parity unpinned; tested
+    against a numpy restatement).  ``cut_outliers`` then uses the column mean of the
+    data before the subtraction.
+    """
     x = _hip.to_device(array)
     out, _ = renormalize_device(x, badchans_mask=badchans_mask, baseline_window=baseline_window,
-                                cut_outliers=cut_outliers)
+                                cut_outliers=cut_outliers, zero_dm=zero_dm)
     return _host(out)
 
 
@@ -227,7 +247,8 @@ def dm_broadening(dm, freq, df):
 
 
 def search_by_chunks(fname, chunk_length=None, new_sample_time=None, tmin=0, dmmin=200, dmmax=800, surelybad=[],
-                     save_candidates=True, snr_threshold=6, acc=None):
+                     save_candidates=True, snr_threshold=6, acc=None, search_dtype="f32", profile=None,
+                     zero_dm=False):
     """clean.py:276-351: stream a SIGPROC file through clean + DM search, chunk by chunk.
 
     Same chunking as the reference: ``step = max(int(chunk_length / tsamp) * 2, 128)``
@@ -238,6 +259,14 @@ def search_by_chunks(fname, chunk_length=None, new_sample_time=None, tmin=0, dmm
     ``N = rint(new_sample_time / tsamp)`` when >= 2; ``dedispersion_search``.  All array
     work stays in HBM (read_block_device -> renormalize_device -> HIP rebin -> search).
 
+    ``search_dtype``: the renormalised chunk is float64 (clean.py:73); ``"f32"``
+    (default) casts it to float32 on the device and searches with the float32 subband
+    kernel (the north star's float32 summation-order tolerance), ``"f64"`` searches the
+    float64 plane with float64 accumulation in channel order (bit-exact series, the
+    slower channel-mode kernel).  ``zero_dm`` is renormalize_data's opt-in subtraction.
+    ``profile``: a list that receives one dict of synchronised per-step timings (ms:
+    h2d, transpose, clean, cast, rebin, search) per chunk.
+
     Returns the list of candidate chunks (max S/N > ``snr_threshold``): dicts with
     istart, iend, t0, best DM, S/N, rebin and the full table.  With ``save_candidates``
     each candidate's PulseInfo is pickled to ``{root}_{istart}-{iend}.pkl`` like the
@@ -246,9 +275,12 @@ def search_by_chunks(fname, chunk_length=None, new_sample_time=None, tmin=0, dmm
     """
     import os
     import pickle
+    import time
     from .dedispersion import _rebin_time_device, delta_delay, search_device
-    from .sigproc import FilReader
+    from .sigproc import FilReader, transpose_device
     from .stats import get_bad_chans
+    if search_dtype not in ("f32", "f64"):
+        raise ValueError(f"search_dtype must be 'f32' or 'f64', got {search_dtype!r}")
     t = _hip.require_gpu()
     fname_root = os.path.basename(fname).split('.')[0]
     mask = get_bad_chans(fname)
@@ -287,20 +319,44 @@ def search_by_chunks(fname, chunk_length=None, new_sample_time=None, tmin=0, dmm
         if chunk_size < step // 2:
             continue
         iend = istart + chunk_size
-        block = fil.read_block_device(istart, chunk_size)
+        marks = []
+
+        def mark(name):
+            if profile is not None:
+                t.cuda.synchronize()
+                marks.append((name, time.perf_counter()))
+
+        mark("start")
+        tc = np.ascontiguousarray(fil._block_tc(istart, chunk_size))
+        src = t.from_numpy(tc).to(t.device("cuda", t.cuda.current_device()))
+        mark("h2d")
+        block = transpose_device(src)
+        del src
+        mark("transpose")
         if _hip.dtype_code(block.dtype) is None:
             block = block.to(t.float64)
-        array, _ = renormalize_device(block, badchans_mask=mask)
+        array, _ = renormalize_device(block, badchans_mask=mask, zero_dm=zero_dm)
+        del block
         if foff < 0:
             array = t.flip(array, dims=(0,)).contiguous()
+        mark("clean")
         if N > 1:
-            array = _rebin_time_device(array, N)
+            array = _rebin_time_device(array, N)  # quick_resample of the float64 plane (clean.py:335-336)
+        mark("rebin")
+        if search_dtype == "f32":
+            array = array.to(t.float32)
+        mark("cast")
         nbin = array.shape[1]
         if trial_DMs is None or plan is None or plan.nsamples != nbin:
             trial_DMs = dedispersion_plan(nchan, dmmin, dmmax, start_freq, bandwidth, new_sample_time)
             plan = None
         (mx, sd, snr, win), plan = search_device(array, trial_DMs, nchan, start_freq, bandwidth, new_sample_time,
                                                  acc=acc, plan=plan)
+        mark("search")
+        if profile is not None:
+            rec = {"istart": istart, "nsamples": chunk_size, "ndm": int(trial_DMs.size)}
+            rec.update({name: (tt - marks[i][1]) * 1e3 for i, (name, tt) in enumerate(marks[1:])})
+            profile.append(rec)
         snr = _host(snr)
         table = make_table({'DM': trial_DMs, 'max': _host(mx), 'std': _host(sd), 'snr': snr, 'rebin': _host(win)})
         if np.any(snr > snr_threshold):

@@ -3,8 +3,11 @@
 The reference's only parallelism is numba ``prange`` over independent DM trials
 (``dedispersion.py:174,181``).  Here the same trial axis is split across ranks:
 
-1. the filterbank is broadcast from ``src`` (RCCL over xGMI; one collective, the
-   data path of the search itself has no other exchange),
+1. the filterbank is broadcast from ``src`` (RCCL over xGMI; the data path of the
+   search itself has no other exchange).  :func:`pipelined_broadcast_search` cuts the
+   broadcast into time chunks and starts the search of each time tile as soon as the
+   columns it reads (its window plus the shift halo) have landed, so the transfer of
+   later chunks overlaps the search of earlier ones;
 2. each rank searches its contiguous slice of the trial grid on its own GPU,
 3. the per-trial statistics (max, std, snr, rebin) are all-gathered, so every rank
    ends with the reference's full-length result arrays.
@@ -35,30 +38,136 @@ def broadcast_filterbank(data, src=0, group=None):
     return data
 
 
+def column_chunks(nsamples, chunks, quantum=1024):
+    """Split [0, nsamples) into about ``chunks`` column ranges (multiples of ``quantum``
+    samples).  Depends on the shape only, so every rank issues the same collectives
+    whatever its plan (plans of different DM slices may use different time tiles)."""
+    n = int(nsamples)
+    width = max(quantum, -(-(-(-n // max(1, int(chunks)))) // quantum) * quantum)
+    return [(c0, min(n, c0 + width)) for c0 in range(0, n, width)]
+
+
+def ready_tiles(plan, landed):
+    """Time tiles whose whole read window lies in the landed column prefix [0, landed)
+    (windows that wrap modulo nsamples wait for the whole array)."""
+    n = plan.nsamples
+    ntt = plan.info["time_tiles"]
+    if landed >= n:
+        return np.ones(ntt, dtype=bool)
+    a0, b0 = plan.tile_window(0)
+    starts = np.arange(ntt, dtype=np.int64) * plan.info["time_tile"]
+    return (starts + a0 >= 0) & (starts + b0 <= landed)
+
+
+def pipelined_broadcast_search(data, plan, out=None, workspace=None, src=0, chunks=8, group=None):
+    """Broadcast ``data`` from ``src`` in time chunks while searching it with ``plan``.
+
+    Chunk k (a range of whole time tiles, all channels) is packed into a contiguous
+    staging buffer on ``src``, RCCL-broadcast on a communication stream and unpacked
+    into ``data`` on the other ranks; every time tile whose read window has landed is
+    searched on a compute stream as soon as its chunk's event fires
+    (pu_plan_search_tiles), and the per-trial outputs are finalised when all tiles ran
+    (pu_plan_finalize).  Returns the (max, std, snr, rebin) device tensors; the caller's
+    current stream is ordered after all of it.  ``plan=None`` (a rank with no trials)
+    only takes part in the broadcasts.
+    """
+    import torch
+    import torch.distributed as dist
+    dev = data.device
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    nchan, n = data.shape
+    bounds = column_chunks(n, chunks)
+    cur = torch.cuda.current_stream(dev)
+    comm = torch.cuda.Stream(device=dev)
+    comp = torch.cuda.Stream(device=dev)
+    comm.wait_stream(cur)
+    comp.wait_stream(cur)
+    if plan is not None:
+        out, workspace = plan._outs_ws(dev, out, workspace)
+        workspace.record_stream(comp)
+        done = np.zeros(plan.info["time_tiles"], dtype=bool)
+    width = max(c1 - c0 for c0, c1 in bounds)
+    staging = torch.empty(nchan * width, dtype=data.dtype, device=dev) if world > 1 else None
+    for c0, c1 in bounds:
+        with torch.cuda.stream(comm):
+            if world > 1:
+                buf = staging[:nchan * (c1 - c0)].view(nchan, c1 - c0)  # contiguous
+                if rank == src:
+                    buf.copy_(data[:, c0:c1])
+                dist.broadcast(buf, src=src, group=group)
+                if rank != src:
+                    data[:, c0:c1].copy_(buf)
+            ev = torch.cuda.Event()
+            ev.record(comm)
+        if plan is None:
+            continue
+        comp.wait_event(ev)
+        ready = ready_tiles(plan, c1) & ~done
+        idx = np.flatnonzero(ready)
+        # contiguous runs of ready tiles, one launch each
+        for run in np.split(idx, np.flatnonzero(np.diff(idx) != 1) + 1) if idx.size else []:
+            plan.search_tiles(data, int(run[0]), int(run[-1]) + 1, workspace, stream=comp)
+        done |= ready
+    if staging is not None:
+        staging.record_stream(comm)
+    cur.wait_stream(comm)
+    if plan is None:
+        return None
+    if not done.all():
+        raise RuntimeError("pipelined search: time tiles left unsearched")
+    plan.finalize(workspace, out=out, stream=comp)
+    for o in out:
+        o.record_stream(comp)
+    cur.wait_stream(comp)
+    return out
+
+
 def sharded_search(data, trial_DMs, nchan, start_freq, bandwidth, sample_time, group=None, acc=None,
-                   compute=None, broadcast=True, src=0):
+                   compute=None, broadcast=True, src=0, pipelined=False, chunks=8):
     """Distributed ``_dedispersion_search``: returns (max, std, snr, rebin[int32]) numpy arrays
     covering ALL trials, on every rank.
 
     ``data`` must be a tensor of the right shape/dtype on every rank (only ``src``'s
-    content matters when ``broadcast``).
+    content matters when ``broadcast``).  ``pipelined`` (HIP compute only) overlaps the
+    broadcast with the search (:func:`pipelined_broadcast_search`).
     """
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    if broadcast and world > 1:
-        broadcast_filterbank(data, src=src, group=group)
     dms = np.asarray(trial_DMs, dtype=np.float64)
     lo, hi = shard_bounds(dms.size, world, rank)
-    fn = compute or (lambda d, t: _hip_compute(d, t, nchan, start_freq, bandwidth, sample_time, acc))
     dev = data.device
     chunk = -(-dms.size // world)  # ceil: equal-size gather buffers
     local = torch.zeros((4, chunk), dtype=torch.float64, device=dev)
-    if hi > lo:
-        res = fn(data, dms[lo:hi])
-        for k in range(4):
-            local[k, :hi - lo] = torch.as_tensor(res[k], dtype=torch.float64, device=dev)
+    if pipelined and compute is None:
+        from . import _hip
+        from .dedispersion import _acc_code, _plan_for, _prepare_data
+        if not (data.is_cuda and data.is_contiguous()):
+            raise ValueError("pipelined sharded_search needs a contiguous device tensor (it is written in place)")
+        x = _prepare_data(data)
+        plan = None
+        if hi > lo:
+            sub = np.ascontiguousarray(dms[lo:hi])
+            plan = _plan_for(x, lambda: _hip.shift_table(nchan, sub, start_freq, bandwidth, sample_time),
+                             _acc_code(acc), ("dm-shard", sub.tobytes(), float(start_freq), float(bandwidth),
+                                              float(sample_time)))
+        if broadcast and world > 1:
+            res = pipelined_broadcast_search(x, plan, src=src, chunks=chunks, group=group)
+        else:
+            res = plan.search(x) if plan is not None else None
+        if res is not None:
+            for k in range(4):
+                local[k, :hi - lo] = res[k].to(torch.float64)
+    else:
+        if broadcast and world > 1:
+            broadcast_filterbank(data, src=src, group=group)
+        fn = compute or (lambda d, t: _hip_compute(d, t, nchan, start_freq, bandwidth, sample_time, acc))
+        if hi > lo:
+            res = fn(data, dms[lo:hi])
+            for k in range(4):
+                local[k, :hi - lo] = torch.as_tensor(res[k], dtype=torch.float64, device=dev)
     parts = [torch.empty_like(local) for _ in range(world)]
     dist.all_gather(parts, local, group=group)
     out = []

@@ -207,6 +207,39 @@ if not have("rebin_in"):
     arrays["roll_shifts"] = sh
     arrays["roll_out"] = D.apply_dm_shifts_to_data(x, sh)
 
+# ---------------------------------------------------------------- clean.dedispersion_search (clean.py:136-180)
+# The PulseInfo route: sample_time = 1 / pulse_freq / nbin (clean.py:141).  The
+# reference writes its plane to ``dummy.npy`` in the CWD (clean.py:150-151): it runs
+# inside a throw-away directory so nothing lands in the repository.
+if not have("pinfo_table_snr"):
+    import tempfile
+
+    class _Info:  # the attributes clean.dedispersion_search reads (clean.py:138-141)
+        pass
+
+    np.random.seed(31)
+    nbin, pulse_freq = 512, 1.7
+    arr, _ = ref.simulate.simulate_test_data(dm=60., tsamp=1 / pulse_freq / nbin, nsamples=nbin, nchan=64,
+                                             start_freq=1200., bandwidth=200.)
+    info = _Info()
+    info.allprofs, info.start_freq, info.bandwidth = arr, 1200., 200.
+    info.pulse_freq, info.nbin = pulse_freq, nbin
+    meta["pinfo_input_sha256"] = sha(arr)
+    cwd = os.getcwd()
+    tmpd = tempfile.mkdtemp()
+    os.chdir(tmpd)
+    try:
+        plane, tab = ref.clean.dedispersion_search(info, 30., 90.)
+        plane = np.array(plane)
+    finally:
+        os.chdir(cwd)
+    meta["pinfo_plane_sha256"] = sha(plane)
+    meta["pinfo_args"] = {"seed": 31, "nbin": nbin, "pulse_freq": pulse_freq, "dm": 60., "nchan": 64,
+                          "start_freq": 1200., "bandwidth": 200., "dmmin": 30., "dmmax": 90.}
+    for col in ("DM", "max", "std", "snr", "rebin"):
+        arrays[f"pinfo_table_{col}"] = np.asarray(tab[col])
+    log("clean.dedispersion_search (PulseInfo)", plane.shape)
+
 # ---------------------------------------------------------------- file statistics (stats.py:35-90)
 # sigpyproc is absent: the reference's get_spectral_stats/get_bad_chans run with their
 # ``FilReader`` name bound to our SIGPROC reader (header/readBlock surface).  What this

@@ -103,6 +103,47 @@ def test_clean_strided_views(gpu, dt, n, pad, off):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("dt", ["f32", "u8"])
+def test_zero_dm_subtraction_c4(gpu, golden, dt):
+    """Opt-in zero-DM subtraction (north_star; no reference counterpart, so parity is
+    unpinned and checked against the numpy restatement in oracle/clean_oracle.py) at C4
+    with the bad channels of get_noisier_channels and the outlier cut; the default path
+    stays the reference's (golden SHA-256)."""
+    import torch
+    from pulsarutils import _hip
+    arrays, meta = golden
+    x = synth.rfi_filterbank_np(CONFIGS["C4"], dtype=dt)
+    bad = C.get_noisier_channels(x)
+    assert bad.any()
+    xd = _hip.to_device(x)
+    out, bins = C.renormalize_device(xd, badchans_mask=bad, cut_outliers=True, zero_dm=True)
+    got = out.cpu().numpy()
+    del out
+    ref, ref_bins = co.renormalize(x, badchans_mask=bad, cut_outliers=True, zero_dm=True, return_badbins=True)
+    np.testing.assert_array_equal(bins, ref_bins)
+    assert np.array_equal(got, ref), np.argwhere(got != ref)[:5]
+    # the subtraction removes the good channels' per-time-bin mean (up to rounding)
+    good = ~bad
+    assert np.abs(got[good].mean(0)).max() < 1e-12
+    assert not got[bad].any()
+    # default (zero_dm=False) is unchanged: the reference's own output
+    out, _ = C.renormalize_device(xd, badchans_mask=bad, cut_outliers=True)
+    assert sha(out.cpu().numpy()) == meta[f"c4{dt}_renorm_cut_sha256"]
+    del out
+    torch.cuda.empty_cache()
+
+
+def test_zero_dm_small_cases(gpu):
+    """Ragged sizes, all channels bad, no channel bad."""
+    rng = np.random.default_rng(13)
+    for nchan, n in [(7, 333), (33, 5000)]:
+        x = (rng.random((nchan, n)) * 5 + 1).astype(np.float32)
+        for bad in (np.zeros(nchan, bool), np.ones(nchan, bool), rng.random(nchan) < 0.3):
+            got = C.renormalize_data(x, badchans_mask=bad, cut_outliers=True, zero_dm=True)
+            want = co.renormalize(x, badchans_mask=bad, cut_outliers=True, zero_dm=True)
+            np.testing.assert_array_equal(got, want)
+
+
 @pytest.mark.parametrize("n", [1, 2, 3, 8, 1001, 4096, 262144, 262145])
 def test_median_device_matches_numpy(gpu, n):
     """np.median (clean.py:80) by device radix select: random, tied, signed-zero,

@@ -34,7 +34,7 @@ def c1_input():
 
 def f32_bound(x, shifts):
     """Per-sample first-order bound nchan * 2^-24 * sum_c |x_c[(t+s_c) mod N]|."""
-    ax = np.abs(x.astype(np.float64))
+    ax = np.abs(x)  # exact in the input dtype; the oracle sums it in float64
     return x.shape[0] * 2.0 ** -24 * oracle.dedisperse(ax, shifts) + 1e-30
 
 
@@ -177,12 +177,13 @@ def test_plane_subband_small_lds_budget(gpu, dt, monkeypatch):
             assert np.all(np.abs(plane[k] - ref) <= f32_bound(x, sh[k])), k
 
 
+@pytest.mark.parametrize("group", [4, 8])
 @pytest.mark.parametrize("shape", ["1", "2"])
 @pytest.mark.parametrize("dt", ["u8", "f32"])
-def test_plane_subband_pair_shape(gpu, dt, shape, monkeypatch):
+def test_plane_subband_pair_shape(gpu, dt, shape, group, monkeypatch):
     """The time-tile-256 subband shapes (PU_SUB_SHAPE=1 pair: 8 waves x 16 trials, two
     workgroups per CU; 2 tall: 16 waves x 16 trials) against the oracle, ragged N and a
-    partial last group (nchan % 4 != 0)."""
+    partial last group (nchan % G != 0 for G = 4 and 8)."""
     c = CONFIGS["C2"]
     rng = np.random.default_rng(33)
     nchan, n = 130, 20000 + 37
@@ -192,8 +193,8 @@ def test_plane_subband_pair_shape(gpu, dt, shape, monkeypatch):
     sh = _hip.shift_table(nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
     monkeypatch.setenv("PU_SUB_SHAPE", shape)
     info = {}
-    plane = _plane(x, sh, "native", 4, info)
-    assert info["group"] == 4 and info["time_tile"] == 256, info
+    plane = _plane(x, sh, "native", group, info)
+    assert info["group"] == group and info["time_tile"] == 256, info
     for k in range(0, 150, 11):
         ref = oracle.dedisperse(x, sh[k])
         if dt == "u8":
@@ -233,6 +234,37 @@ def test_search_slow_path_plane(gpu, golden):
     np.testing.assert_array_equal(tab["rebin"], arrays["test_slow_table_rebin"])
     np.testing.assert_allclose(tab["snr"], arrays["test_slow_table_snr"], rtol=1e-9)
     assert np.isclose(tab["DM"][np.argmax(tab["snr"])], 150, atol=1)
+
+
+def pinfo_case(meta):
+    """The PulseInfo input of the clean.dedispersion_search golden (make_golden.py)."""
+    from pulsarutils.clean import PulseInfo
+    a = meta["pinfo_args"]
+    np.random.seed(a["seed"])
+    arr, _ = simulate.simulate_test_data(dm=a["dm"], tsamp=1 / a["pulse_freq"] / a["nbin"], nsamples=a["nbin"],
+                                         nchan=a["nchan"], start_freq=a["start_freq"], bandwidth=a["bandwidth"])
+    assert sha(arr) == meta["pinfo_input_sha256"]
+    info = PulseInfo()
+    info.allprofs, info.start_freq, info.bandwidth = arr, a["start_freq"], a["bandwidth"]
+    info.pulse_freq, info.nbin, info.nchan = a["pulse_freq"], a["nbin"], a["nchan"]
+    return info, a
+
+
+def test_clean_dedispersion_search_pulseinfo(gpu, golden):
+    """clean.dedispersion_search(info, dmmin, dmmax) (clean.py:136-180): the PulseInfo
+    route (sample_time = 1 / pulse_freq / nbin), float64 plane bit-identical to the
+    reference's ``dummy.npy`` memmap, table equal to the reference's (rebin int64)."""
+    from pulsarutils import clean as C
+    arrays, meta = golden
+    info, a = pinfo_case(meta)
+    plane, tab = C.dedispersion_search(info, a["dmmin"], a["dmmax"])
+    assert plane.dtype == np.float64 and plane.shape == (arrays["pinfo_table_DM"].size, a["nbin"])
+    assert sha(plane) == meta["pinfo_plane_sha256"]
+    np.testing.assert_array_equal(tab["DM"], arrays["pinfo_table_DM"])
+    for col in ("max", "std", "snr"):
+        np.testing.assert_allclose(tab[col], arrays[f"pinfo_table_{col}"], rtol=1e-9, atol=1e-12)
+    np.testing.assert_array_equal(tab["rebin"], arrays["pinfo_table_rebin"])
+    assert tab["rebin"].dtype == np.int64
 
 
 def test_search_c1_vs_reference(gpu, golden):
@@ -291,24 +323,49 @@ def test_search_full_size_sampled_trials(gpu, golden, name):
     best = dms[np.argmax(snr)]
     assert abs(best - c.pulse_dm) < 0.5, (best, c.pulse_dm)
     x = xd.cpu().numpy()
-    idx = np.unique(np.r_[np.linspace(0, dms.size - 1, 6).astype(int), np.argmax(snr)])
+    idx = sampled_trials(snr, 32)
     omx, osd, osnr, owin = oracle.search(x, dms[idx], c.start_freq, c.bandwidth, c.tsamp, nthreads=16)
     np.testing.assert_allclose(snr[idx], osnr, rtol=1e-5)
     np.testing.assert_allclose(sd.cpu().numpy()[idx], osd, rtol=1e-5)
     np.testing.assert_allclose(mx.cpu().numpy()[idx], omx, rtol=1e-4, atol=1e-3)
     np.testing.assert_array_equal(win.cpu().numpy()[idx], owin)
+    # argmax DM over the sample agrees (the top 5 by S/N are in it)
+    assert idx[np.argmax(snr[idx])] == idx[np.argmax(osnr)]
+
+
+def sampled_trials(snr, n):
+    """About ``n`` trials: evenly spaced ones plus the top 5 by S/N (where argmax-DM and
+    rebin equality matter)."""
+    top = np.argsort(snr)[::-1][:5]
+    return np.unique(np.r_[np.linspace(0, snr.size - 1, n - 5).astype(int), top])
 
 
 @pytest.mark.parametrize("name,group", [("C2", 4), ("C3", 8), ("C5", 4)])
 def test_default_group_cost_model(gpu, golden, name, group):
     """With no explicit group the planner keeps the cheaper of G = 8 / G = 4 by its cost
-    model; at C2/C3/C5 that is the measured winner (profiles/r01_autog/)."""
+    model; at C2/C3/C5 that is the measured winner (profiles/r01_autog/).  The default
+    plan's dedispersed rows also match the oracle (float32: the summation-order bound;
+    uint8: bit-exact), so the numerics do not depend on which G the model picks."""
+    import torch
+    from pulsarutils import synth
     c = CONFIGS[name]
     dms = D.dedispersion_plan(c.nchan, c.dmmin, c.dmmax, c.start_freq, c.bandwidth, c.tsamp)
     sh = _hip.shift_table(c.nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
     code = {"u8": _hip.PU_U8, "f32": _hip.PU_F32}[c.dtype]
-    info = _hip.Plan(code, _hip.PU_ACC_NATIVE, c.nchan, c.nsamples, sh).info
-    assert info["group"] == group, info
+    plan = _hip.Plan(code, _hip.PU_ACC_NATIVE, c.nchan, c.nsamples, sh)
+    assert plan.info["group"] == group, plan.info
+    if name == "C3":
+        return  # C3's default-plan rows are checked bit-exact in test_search_c3_full_size_u8
+    xd = synth.pulsar_filterbank_device(c)
+    plane = plan.dedisperse(xd)
+    idx = np.array([0, dms.size // 3, dms.size - 1])
+    rows = plane[torch.as_tensor(idx, device=xd.device)].cpu().numpy()
+    del plane
+    torch.cuda.empty_cache()
+    x = xd.cpu().numpy()
+    for k, i in enumerate(idx):
+        ref = oracle.dedisperse(x, sh[i])
+        assert np.all(np.abs(rows[k] - ref) <= f32_bound(x, sh[i])), i
 
 
 def test_plan_cache_reuse(gpu, monkeypatch):
@@ -361,10 +418,15 @@ def test_search_c3_full_size_u8(gpu):
                                              nthreads=16, return_dedisp=True)
     for k in range(idx.size):
         np.testing.assert_array_equal(plane[k].astype(np.float64), dd[k])
+    del dd
+    # statistics of ~32 trials (evenly spaced + the top 5 by S/N): argmax DM and rebin pinned
+    idx = sampled_trials(snr, 32)
+    omx, osd, osnr, owin = oracle.search(x, dms[idx], c.start_freq, c.bandwidth, c.tsamp, nthreads=16)
     np.testing.assert_allclose(snr[idx], osnr, rtol=1e-5)
     np.testing.assert_allclose(sd.cpu().numpy()[idx], osd, rtol=1e-5)
     np.testing.assert_allclose(mx.cpu().numpy()[idx], omx, rtol=1e-5)
     np.testing.assert_array_equal(win.cpu().numpy()[idx], owin)
+    assert idx[np.argmax(snr[idx])] == idx[np.argmax(osnr)]
 
 
 def test_search_u8_bitexact_series_c3_slice(gpu):
@@ -385,11 +447,13 @@ def test_search_u8_bitexact_series_c3_slice(gpu):
     torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("group", [4, 8])
 @pytest.mark.parametrize("shape", ["0", "1", "2"])
-def test_plane_u8_dma_rows(gpu, shape, monkeypatch):
+def test_plane_u8_dma_rows(gpu, shape, group, monkeypatch):
     """8-bit rows staged by LDS-DMA (N % 4 == 0): bit-exact against the oracle and the
-    global-read build (PU_U8_DMA=0), with a partial last group, row misalignments
-    (base % 4 != 0), a padded row stride and a view whose rows are not 4-byte aligned."""
+    global-read build (PU_U8_DMA=0), with a partial last group (130 % G != 0), row
+    misalignments (base % 4 != 0), a padded row stride and a view whose rows are not
+    4-byte aligned."""
     import torch
     c = CONFIGS["C2"]
     rng = np.random.default_rng(44)
@@ -398,14 +462,14 @@ def test_plane_u8_dma_rows(gpu, shape, monkeypatch):
     dms = np.linspace(0.0, 60.0, 150)
     sh = _hip.shift_table(nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
     monkeypatch.setenv("PU_SUB_SHAPE", shape)
-    plan = _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, nchan, n, sh, group=4)
-    assert plan.info["group"] == 4, plan.info
+    plan = _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, nchan, n, sh, group=group)
+    assert plan.info["group"] == group, plan.info
     xd = _hip.to_device(x)
     plane = plan.dedisperse(xd).cpu().numpy()
     for k in range(0, 150, 13):
         np.testing.assert_array_equal(plane[k].astype(np.float64), oracle.dedisperse(x, sh[k]))
     monkeypatch.setenv("PU_U8_DMA", "0")
-    ref = _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, nchan, n, sh, group=4).dedisperse(xd).cpu().numpy()
+    ref = _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, nchan, n, sh, group=group).dedisperse(xd).cpu().numpy()
     np.testing.assert_array_equal(plane, ref)
     monkeypatch.delenv("PU_U8_DMA")
     big = torch.zeros((nchan, n + 8), dtype=torch.uint8, device=xd.device)
@@ -414,3 +478,51 @@ def test_plane_u8_dma_rows(gpu, shape, monkeypatch):
     np.testing.assert_array_equal(plan.dedisperse(big[:, 1:1 + n].copy_(xd)).cpu().numpy(), plane)  # copied
     g = plan.search(big[:, 1:1 + n])
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("group", [4, 8])
+def test_plane_u8_global_rows_ragged(gpu, group):
+    """8-bit rows read from global memory (N % 4 != 0: no LDS-DMA) with a partial last
+    group (nchan % G != 0): bit-exact against the oracle."""
+    c = CONFIGS["C2"]
+    rng = np.random.default_rng(45)
+    nchan, n = 130, 20001
+    x = (rng.random((nchan, n)) * 60).astype(np.uint8)
+    dms = np.linspace(0.0, 60.0, 150)
+    sh = _hip.shift_table(nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
+    info = {}
+    plane = _plane(x, sh, "native", group, info)
+    assert info["group"] == group, info
+    for k in range(0, 150, 13):
+        np.testing.assert_array_equal(plane[k].astype(np.float64), oracle.dedisperse(x, sh[k]))
+
+
+@pytest.mark.parametrize("dt", ["u8", "f32"])
+def test_default_group_ragged_vs_oracle(gpu, dt):
+    """No explicit group (automatic G = 4 / 8 choice) at a ragged nchan: the plan the
+    planner keeps is reported, and its plane and search match the oracle."""
+    c = CONFIGS["C2"]
+    rng = np.random.default_rng(46)
+    nchan, n = 203, 40000
+    x = rng.random((nchan, n)) * 40
+    x = x.astype(np.uint8) if dt == "u8" else x.astype(np.float32)
+    dms = np.linspace(0.0, 60.0, 300)
+    sh = _hip.shift_table(nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
+    info = {}
+    plane = _plane(x, sh, "native", 0, info)
+    assert info["group"] in (4, 8), info
+    for k in range(0, 300, 23):
+        ref = oracle.dedisperse(x, sh[k])
+        if dt == "u8":
+            np.testing.assert_array_equal(plane[k].astype(np.float64), ref)
+        else:
+            assert np.all(np.abs(plane[k] - ref) <= f32_bound(x, sh[k])), k
+    g = D._dedispersion_search(x, dms, nchan, c.start_freq, c.bandwidth, c.tsamp)
+    o = oracle.search(x, dms, c.start_freq, c.bandwidth, c.tsamp, nthreads=16)
+    for a, b in zip(g[:3], o[:3]):
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-9)
+    np.testing.assert_array_equal(g[3], o[3])
+    for forced in (4, 8):
+        pf = _plane(x, sh, "native", forced)
+        if dt == "u8":
+            np.testing.assert_array_equal(pf, plane)

@@ -38,9 +38,11 @@ def test_spectral_stats_and_bad_chans(gpu, golden, tmp_path, dt):
     np.testing.assert_array_equal(stats.get_bad_chans(fname), bad)
 
 
-def test_search_by_chunks_finds_pulse(gpu, tmp_path, monkeypatch):
+@pytest.mark.parametrize("search_dtype", ["f64", "f32"])
+def test_search_by_chunks_finds_pulse(gpu, tmp_path, monkeypatch, search_dtype):
     """A dispersed pulse in a foff<0 u8 file: found in the chunks covering it, and each
-    chunk table equals the oracle composition of the reference steps."""
+    chunk table equals the oracle composition of the reference steps (float64 search:
+    1e-9; float32 search of the float32-cast plane: 1e-5)."""
     from pulsarutils import clean, _planner
     nch, ns, tsamp = 64, 20000, 2e-4
     fch1, foff = 1500.0, -300.0 / nch
@@ -55,17 +57,22 @@ def test_search_by_chunks_finds_pulse(gpu, tmp_path, monkeypatch):
     fname = str(tmp_path / "pulse.fil")
     sigproc.write_filterbank(fname, x, fch1=fch1, foff=foff, tsamp=tsamp)
     monkeypatch.chdir(tmp_path)
-    cands = clean.search_by_chunks(fname, dmmin=250, dmmax=350, new_sample_time=tsamp, save_candidates=True)
+    prof = []
+    cands = clean.search_by_chunks(fname, dmmin=250, dmmax=350, new_sample_time=tsamp, save_candidates=True,
+                                   search_dtype=search_dtype, profile=prof)
     assert cands, "pulse not found"
+    assert prof and all(k in prof[0] for k in ("h2d", "transpose", "clean", "rebin", "cast", "search"))
     best = max(cands, key=lambda c: c["snr"])
     assert abs(best["dm"] - 300) < 3 and best["istart"] <= 9000 < best["iend"]
     assert os.path.exists(f"pulse_{best['istart']}-{best['iend']}.pkl")
     # oracle composition for that chunk: get_bad_chans -> renormalize -> flip -> search
     mask = np.loadtxt(fname + ".badchans").astype(bool)
     blk = sigproc.FilReader(fname).readBlock(best["istart"], best["iend"] - best["istart"])
-    ren = co.renormalize(blk, badchans_mask=mask)[::-1]
+    ren = np.ascontiguousarray(co.renormalize(blk, badchans_mask=mask)[::-1])
+    if search_dtype == "f32":
+        ren = ren.astype(np.float32)
     dms = dedispersion_plan(nch, 250, 350, fbottom, 300.0, tsamp)
-    omx, osd, osnr, owin = oracle.search(np.ascontiguousarray(ren), dms, fbottom, 300.0, tsamp)
+    omx, osd, osnr, owin = oracle.search(ren, dms, fbottom, 300.0, tsamp)
     tab = best["table"]
-    np.testing.assert_allclose(tab["snr"], osnr, rtol=1e-9)
+    np.testing.assert_allclose(tab["snr"], osnr, rtol=1e-9 if search_dtype == "f64" else 1e-5)
     np.testing.assert_array_equal(tab["rebin"], owin)

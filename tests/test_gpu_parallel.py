@@ -1,0 +1,83 @@
+"""The multi-GPU product path on one GPU: the HIP compute of ``parallel.sharded_search``
+under a world-size-1 RCCL (nccl) process group, and the pipelined broadcast + search
+(time-tile range launches, pu_plan_search_tiles + pu_plan_finalize) against the one-shot
+search.  The multi-rank split / broadcast / gather plumbing is covered on CPU by
+tests/test_parallel_gloo.py (gloo, world 2-4)."""
+import socket
+
+import numpy as np
+import pytest
+
+import oracle
+from pulsarutils import _hip, parallel, synth
+from pulsarutils import dedispersion as D
+from pulsarutils.configs import CONFIGS
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("name,chunks", [("C5", 5), ("C2s", 8), ("C3s", 3)])
+def test_pipelined_tiles_equal_full_search(gpu, name, chunks):
+    """Searching time-tile ranges as chunks land, then finalising, gives the one-shot
+    pu_plan_search outputs bit for bit (same kernels, same per-tile records, same
+    deterministic finalize order); wrapping tiles wait for the last chunk."""
+    import torch
+    from dataclasses import replace
+    c = {"C5": CONFIGS["C5"], "C2s": replace(CONFIGS["C2"], nchan=256, nsamples=1 << 18),
+         "C3s": replace(CONFIGS["C3"], nchan=512, nsamples=1 << 18)}[name]
+    xd = synth.pulsar_filterbank_device(c)
+    dms = D.dedispersion_plan(c.nchan, c.dmmin, c.dmmax, c.start_freq, c.bandwidth, c.tsamp)[:300]
+    sh = _hip.shift_table(c.nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
+    plan = _hip.Plan(_hip.dtype_code(xd.dtype), _hip.PU_ACC_NATIVE, c.nchan, c.nsamples, sh)
+    full = [o.cpu().numpy() for o in plan.search(xd)]
+    piped = [o.cpu().numpy() for o in parallel.pipelined_broadcast_search(xd, plan, chunks=chunks)]
+    torch.cuda.synchronize()
+    for a, b in zip(full, piped):
+        np.testing.assert_array_equal(a, b)
+    # tile-range launches with an empty and a partial range, finalised
+    ws = torch.empty(plan.workspace_bytes, dtype=torch.uint8, device=xd.device)
+    ntt = plan.info["time_tiles"]
+    plan.search_tiles(xd, 0, 0, ws)
+    plan.search_tiles(xd, ntt // 3, ntt, ws)
+    plan.search_tiles(xd, 0, ntt // 3, ws)
+    for a, b in zip(full, plan.finalize(ws)):
+        np.testing.assert_array_equal(a, b.cpu().numpy())
+    with pytest.raises(ValueError):
+        plan.search_tiles(xd, 0, ntt + 1, ws)
+
+
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_sharded_search_nccl_world1(gpu, pipelined):
+    """parallel.sharded_search with the HIP compute (the product path) under a real
+    RCCL process group of size 1: equals the single-process search, and the sampled
+    trials equal the oracle within SURVEY §8a's 1e-5."""
+    import torch
+    import torch.distributed as dist
+    from dataclasses import replace
+    c = replace(CONFIGS["C2"], nchan=256, nsamples=1 << 17)
+    xd = synth.pulsar_filterbank_device(c)
+    dms = D.dedispersion_plan(c.nchan, c.dmmin, c.dmmax, c.start_freq, c.bandwidth, c.tsamp)[:257]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=xd.device)
+    try:
+        mx, sd, snr, win = parallel.sharded_search(xd, dms, c.nchan, c.start_freq, c.bandwidth, c.tsamp,
+                                                   pipelined=pipelined)
+    finally:
+        dist.destroy_process_group()
+    ref = D._dedispersion_search(xd, dms, c.nchan, c.start_freq, c.bandwidth, c.tsamp)
+    for a, b in zip((mx, sd, snr, win), ref):
+        np.testing.assert_array_equal(a, b)
+    assert win.dtype == np.int32
+    idx = np.unique(np.r_[np.linspace(0, dms.size - 1, 8).astype(int), np.argmax(snr)])
+    o = oracle.search(xd.cpu().numpy(), dms[idx], c.start_freq, c.bandwidth, c.tsamp, nthreads=16)
+    np.testing.assert_allclose(snr[idx], o[2], rtol=1e-5)
+    np.testing.assert_array_equal(win[idx], o[3])
+    torch.cuda.synchronize()

@@ -74,6 +74,29 @@ def test_oracle_search_bitexact_test_config(golden):
     assert np.isclose(arrays["test_table_DM"][np.argmax(snr)], 150, atol=1)
 
 
+def test_oracle_pulseinfo_search_and_plane(golden):
+    """clean.dedispersion_search's PulseInfo route (clean.py:136-180): grid, plane
+    (dedisperse per trial, float64) and table of the oracle equal the reference's."""
+    import hashlib
+    from pulsarutils.dedispersion import dedispersion_plan
+    arrays, meta = golden
+    a = meta["pinfo_args"]
+    np.random.seed(a["seed"])
+    tsamp_sim = 1 / a["pulse_freq"] / a["nbin"]
+    arr, _ = simulate.simulate_test_data(dm=a["dm"], tsamp=tsamp_sim, nsamples=a["nbin"], nchan=a["nchan"],
+                                         start_freq=a["start_freq"], bandwidth=a["bandwidth"])
+    assert sha(arr) == meta["pinfo_input_sha256"]
+    sample_time = 1 / a["pulse_freq"] / a["nbin"]  # clean.py:141
+    dms = dedispersion_plan(a["nchan"], a["dmmin"], a["dmmax"], a["start_freq"], a["bandwidth"], sample_time)
+    np.testing.assert_array_equal(dms, arrays["pinfo_table_DM"])
+    plane = np.array([oracle.dedisperse(arr, oracle.shifts(a["nchan"], dm, a["start_freq"], a["bandwidth"],
+                                                           sample_time)) for dm in dms])
+    assert hashlib.sha256(plane.tobytes()).hexdigest() == meta["pinfo_plane_sha256"]
+    mx, sd, snr, win = oracle.search(arr, dms, a["start_freq"], a["bandwidth"], sample_time)
+    for got, col in zip((mx, sd, snr, win), ("max", "std", "snr", "rebin")):
+        np.testing.assert_array_equal(got, arrays[f"pinfo_table_{col}"])
+
+
 @pytest.mark.parametrize("dt", [np.float32, np.float64])
 @pytest.mark.parametrize("n", [5, 127, 129, 1000, 8192, 8193, 20000, 65536 + 77])
 def test_numpy_order_emulation(dt, n):

@@ -1,4 +1,5 @@
-"""Multi-process DM sharding on CPU (gloo, world_size 2): the shard split, the filterbank
+"""Multi-process DM sharding on CPU (gloo, world_size 2-4, uneven shards and ranks with no
+trials): the shard split, the filterbank
 broadcast and the statistics all-gather reproduce the single-process search exactly.
 The per-shard compute is the oracle here (no GPU on this host); on GPUs it is the HIP search."""
 import os
@@ -60,14 +61,14 @@ WORKER = textwrap.dedent("""
 """)
 
 
-@pytest.mark.parametrize("ndm", [37, 3])
-def test_sharded_search_gloo_world2(tmp_path, ndm):
+@pytest.mark.parametrize("world,ndm", [(2, 37), (2, 3), (3, 37), (3, 2), (4, 38), (4, 3)])
+def test_sharded_search_gloo(tmp_path, world, ndm):
     script = tmp_path / "worker.py"
     script.write_text(WORKER.format(pkg=PKG_DIR, repo=REPO, ndm=ndm))
     port = _free_port()
     procs = []
-    for rank in range(2):
-        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2",
+    for rank in range(world):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                    LOCAL_RANK=str(rank), OMP_NUM_THREADS="1")
         procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT, text=True))
@@ -82,3 +83,51 @@ def test_sharded_search_gloo_world2(tmp_path, ndm):
     for p, out in zip(procs, outs):
         assert p.returncode == 0, out
         assert "ok" in out
+
+
+class _FakePlan:
+    """The attributes ready_tiles reads (a pu_plan's time tiling + shift extent)."""
+
+    def __init__(self, nsamples, tt_len, shift_min, shift_max, max_spread):
+        self.nsamples = nsamples
+        self.info = {"time_tile": tt_len, "time_tiles": -(-nsamples // tt_len), "max_spread": max_spread}
+        self.shift_min, self.shift_max = shift_min, shift_max
+
+    def tile_window(self, tt):
+        from pulsarutils._hip import Plan
+        return Plan.tile_window(self, tt)
+
+
+@pytest.mark.parametrize("n,chunks", [(1 << 22, 8), (1 << 20, 3), (12345, 4), (1000, 8)])
+def test_column_chunks_rank_independent(n, chunks):
+    """The chunked broadcast's column ranges depend on the shape only (every rank issues
+    the same collectives whatever its plan), cover [0, n) and are whole quanta."""
+    from pulsarutils.parallel import column_chunks
+    b = column_chunks(n, chunks)
+    assert b[0][0] == 0 and b[-1][1] == n
+    assert all(c1 == d0 for (_, c1), (d0, _) in zip(b, b[1:]))
+    assert all((c1 - c0) % 1024 == 0 for c0, c1 in b[:-1])
+    assert len(b) <= max(1, chunks)
+
+
+@pytest.mark.parametrize("shift_min,shift_max", [(-2084, 2914), (0, 582), (-843, 1931)])
+def test_ready_tiles_halo(shift_min, shift_max):
+    """A time tile is searched only once its whole read window (shift halo + LDS-DMA
+    rounding) has landed; tiles whose window wraps modulo N wait for the last chunk;
+    every tile is ready at the end."""
+    from pulsarutils.parallel import column_chunks, ready_tiles
+    n, tt_len = 1 << 20, 512
+    plan = _FakePlan(n, tt_len, shift_min, shift_max, 74)
+    seen = np.zeros(plan.info["time_tiles"], dtype=bool)
+    for _, c1 in column_chunks(n, 8):
+        r = ready_tiles(plan, c1)
+        assert not (seen & ~r).any()  # monotone in the landed prefix
+        for tt in np.flatnonzero(r & ~seen):
+            a, b = plan.tile_window(tt)
+            assert c1 >= n or (a >= 0 and b <= c1)
+            # the kernel's own reads: [t0 + smin, t0 + TT + smax + spread + 1 + DMA rounding)
+            assert a <= tt * tt_len + shift_min and b >= (tt + 1) * tt_len + shift_max + 74 + 1 + 256
+        seen |= r
+    assert seen.all()
+    if shift_min < 0:
+        assert not ready_tiles(plan, n - 1)[0]  # tile 0 wraps to the end of the array
