@@ -182,6 +182,20 @@ int pu_renorm_apply_zero_dm(const void *x, int dtype, int64_t nchan, int64_t n, 
                             int64_t ngood, double *out, int64_t ld_out, double *col_means,
                             void *stream);
 
+/* cut_outliers of renormalize_data (clean.py:93-105) on the device: from the column
+ * means lc[n] of the renormalised plane (pu_renorm_apply's col_means), mask[t] =
+ * uniform_filter1d(lc, 16)[t] > 5 sd  or  < -3 sd, sd = np.std(uniform_filter1d(lc,
+ * 16)[::16]), and out[:, t] = 0 where mask[t].  scipy's running-sum order is not
+ * reproducible in parallel: every decision is made on directly summed windows and
+ * CERTIFIED against a rigorous rounding bound of both orders; a decision closer to
+ * its threshold than the bound (or a NaN) sets the flag word ws[0:4] (uint32) and the
+ * caller must redo the step on the host (scipy) from a fresh apply pass.  ws[4:8]
+ * (uint32) = number of bad bins.  n >= 64; ws: pu_cut_outliers_workspace_bytes(n),
+ * 8-byte aligned. */
+size_t pu_cut_outliers_workspace_bytes(int64_t n);
+int pu_cut_outliers(const double *lc, int64_t n, double *out, int64_t nrows, int64_t ld_out,
+                    uint8_t *mask, void *workspace, size_t workspace_bytes, void *stream);
+
 /* out[:, cols[k]] = 0 for k < ncols (clean.py:105). cols: device int64. */
 int pu_zero_columns(double *out, int64_t nrows, int64_t ld_out, const int64_t *cols,
                     int64_t ncols, void *stream);

@@ -225,10 +225,10 @@ constexpr int kMaxBatchRows = 32;
 // Rows [0, rn) of a column strip, in order: batches of U rows alternate between two
 // register buffers, the next batch's loads issued before the current batch is
 // consumed (no register copies, so a wait never covers the batch in flight).
-template <typename Tin, int V, typename Body>
+template <typename Tin, int V, typename Body, int BB = kBatchBytes>
 __device__ __forceinline__ void walk_rows(const Tin *p, int64_t ld, int rn, Body &&body)
 {
-    constexpr int U = std::max(1, std::min(kMaxBatchRows, kBatchBytes / (V * (int)sizeof(Tin))));
+    constexpr int U = std::max(1, std::min(kMaxBatchRows, BB / (V * (int)sizeof(Tin))));
     Vec<Tin, V> a[U], b[U];
     auto load = [&](Vec<Tin, V>(&dst)[U], int i0) {
         if (i0 + U <= rn) {
@@ -262,7 +262,7 @@ __device__ __forceinline__ void walk_rows(const Tin *p, int64_t ld, int rn, Body
 // Skipped rows add +0.0 (a select, not a branch): acc starts at +0.0 and never
 // becomes -0.0 under round-to-nearest, so acc + 0.0 == acc bit for bit, and NaN or
 // Inf in a skipped row never reaches the sum.
-template <typename Tin, int V>
+template <typename Tin, int V, int BB>
 __global__ void __launch_bounds__(256)
 colmean_kernel(const Tin *__restrict__ x, int64_t nrows, int64_t col0, int64_t ncols, int64_t ld,
                const uint8_t *__restrict__ skip, double *__restrict__ out)
@@ -274,6 +274,11 @@ colmean_kernel(const Tin *__restrict__ x, int64_t nrows, int64_t col0, int64_t n
 #pragma unroll
     for (int j = 0; j < V; ++j) acc[j] = 0.0;
     int64_t ngood = 0;
+    auto body_fn = [&](int i, const Vec<Tin, V> &v) {
+        const bool s = sk[i] != 0;
+#pragma unroll
+        for (int j = 0; j < V; ++j) acc[j] += s ? 0.0 : static_cast<double>(v.v[j]);
+    };
     for (int64_t r0 = 0; r0 < nrows; r0 += kRowChunk) {
         const int rn = (int)(nrows - r0 < kRowChunk ? nrows - r0 : kRowChunk);
         __syncthreads();
@@ -281,11 +286,7 @@ colmean_kernel(const Tin *__restrict__ x, int64_t nrows, int64_t col0, int64_t n
         __syncthreads();
         for (int i = 0; i < rn; ++i) ngood += sk[i] ? 0 : 1;
         if (!active) continue;
-        walk_rows<Tin, V>(x + r0 * ld + c, ld, rn, [&](int i, const Vec<Tin, V> &v) {
-            const bool s = sk[i] != 0;
-#pragma unroll
-            for (int j = 0; j < V; ++j) acc[j] += s ? 0.0 : static_cast<double>(v.v[j]);
-        });
+        walk_rows<Tin, V, decltype(body_fn) &, BB>(x + r0 * ld + c, ld, rn, body_fn);
     }
     if (!active) return;
 #pragma unroll
@@ -434,6 +435,144 @@ apply_kernel(const Tin *__restrict__ x, int64_t nchan, int64_t col0, int64_t nco
     for (int j = 0; j < V; ++j) col_means[c + j] = acc[j] / static_cast<double>(nchan);
 }
 
+// ---------------------------------------------------------------- cut_outliers
+// clean.py:93-105 on the device.  Only the last window (16) of the reference loop
+// survives: lc_rebin = uniform_filter1d(lc, 16) (mode reflect: window [i-8, i+7]),
+// sd = np.std(lc_rebin[::16]), bad = lc_rebin > 5 sd | lc_rebin < -3 sd.
+//
+// scipy evaluates lc_rebin as a sequential running sum (tmp += (x[i+7] - x[i-9]) / 16),
+// a chain no parallel order reproduces bit for bit.  The kernels instead compute each
+// window sum directly (u[i]) and CERTIFY every decision: with L = max |lc|, both the
+// chain value v[i] and u[i] lie within (2n + 64) 2^-53 L of the exact windowed mean
+// (per-step rounding of the chain <= 1.5 2^-53 L, of the 16-term sum <= 16 2^-53 L),
+// and |std(u) - std(v)| <= max |u - v| plus rounding.  A comparison is decided only
+// when u is farther than that bound from the threshold; otherwise (or on NaN) the
+// state's flag is raised and the host redoes the step with scipy itself.  So the mask
+// equals the reference's bit for bit whenever the flag is clear.
+struct OutlierState {
+    uint32_t flag;             // 1: a decision was ambiguous or a value NaN (ABI: bytes 0-3)
+    uint32_t nbad;             // bad time bins (ABI: bytes 4-7)
+    unsigned long long lbits;  // max |lc| as ordered bits (non-negative doubles)
+    double sd;
+    double up, down;           // 5 sd, -3 sd
+    double margin_up, margin_down;
+};
+
+__device__ __forceinline__ int64_t reflect_small(int64_t i, int64_t n)
+{
+    // scipy 'reflect' for |offset| <= n (windows of 16 at the ends)
+    if (i < 0) i = -i - 1;
+    if (i >= n) i = 2 * n - 1 - i;
+    return i < 0 ? 0 : (i >= n ? n - 1 : i);
+}
+
+__global__ void __launch_bounds__(256)
+outlier_window_kernel(const double *__restrict__ lc, int64_t n, double *__restrict__ u, OutlierState *st)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    double s = 0.0, a = 0.0;
+    bool nan = false;
+    if (i < n) {
+        for (int j = -8; j < 8; ++j) s += lc[(i + j >= 0 && i + j < n) ? i + j : reflect_small(i + j, n)];
+        u[i] = s / 16.0;
+        const double x = lc[i];
+        nan = x != x;
+        a = fabs(x);
+    }
+    // block max of |lc| (non-negative doubles order like their bit patterns)
+    unsigned long long b = nan ? ~0ull : (unsigned long long)__double_as_longlong(a);
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(b, off, 64);
+        b = o > b ? o : b;
+    }
+    __shared__ unsigned long long wm[4];
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long m = wm[0];
+        for (int w = 1; w < 4; ++w) m = wm[w] > m ? wm[w] : m;
+        if (m == ~0ull) atomicOr(&st->flag, 1u);
+        else atomicMax(&st->lbits, m);
+    }
+}
+
+// One workgroup: sd = std(u[::16]) (two passes), thresholds and certification margins.
+__global__ void __launch_bounds__(1024) outlier_std_kernel(const double *__restrict__ u, int64_t n, OutlierState *st)
+{
+    __shared__ double red[1024];
+    const int t = threadIdx.x;
+    const int64_t m = (n + 15) / 16;
+    double s = 0.0;
+    for (int64_t k = t; k < m; k += 1024) s += u[16 * k];
+    red[t] = s;
+    __syncthreads();
+    for (int w = 512; w > 0; w >>= 1) {
+        if (t < w) red[t] += red[t + w];
+        __syncthreads();
+    }
+    const double mean = red[0] / (double)m;
+    __syncthreads();
+    s = 0.0;
+    for (int64_t k = t; k < m; k += 1024) {
+        const double d = u[16 * k] - mean;
+        s += d * d;
+    }
+    red[t] = s;
+    __syncthreads();
+    for (int w = 512; w > 0; w >>= 1) {
+        if (t < w) red[t] += red[t + w];
+        __syncthreads();
+    }
+    if (t == 0) {
+        const double sd = sqrt(red[0] / (double)m);
+        const double L = __longlong_as_double((long long)st->lbits);
+        const double E = ((double)(2 * n + 64) * 0x1p-53) * L + 1e-300;  // |u - v| bound
+        const double Es = E + 1e-12 * sd;                                  // |std(u) - std(v)| bound
+        st->sd = sd;
+        st->up = 5.0 * sd;
+        st->down = -3.0 * sd;
+        st->margin_up = E + 5.0 * Es + 1e-15 * (L + 5.0 * sd);
+        st->margin_down = E + 3.0 * Es + 1e-15 * (L + 3.0 * sd);
+        if (sd != sd) st->flag |= 1u;
+    }
+}
+
+// Per 64 columns: wave 0 decides (certified) and records the mask; then the block
+// zeroes the bad columns of the plane (rows strided over the 4 waves).
+__global__ void __launch_bounds__(256)
+outlier_mask_zero_kernel(const double *__restrict__ u, int64_t n, OutlierState *st, uint8_t *__restrict__ mask,
+                         double *__restrict__ out, int64_t nrows, int64_t ld)
+{
+    __shared__ uint8_t bad[64];
+    __shared__ int any;
+    const int64_t c0 = (int64_t)blockIdx.x * 64;
+    const int t = threadIdx.x;
+    if (t == 0) any = 0;
+    __syncthreads();
+    if (t < 64) {
+        const int64_t i = c0 + t;
+        uint8_t b = 0;
+        if (i < n) {
+            const double v = u[i];
+            const double du = v - st->up, dd = v - st->down;
+            const bool amb = !(fabs(du) > st->margin_up) || !(fabs(dd) > st->margin_down);
+            if (amb) atomicOr(&st->flag, 1u);
+            b = (du > 0.0 || dd < 0.0) ? 1 : 0;
+            mask[i] = b;
+            if (b) {
+                atomicAdd(&st->nbad, 1u);
+                any = 1;
+            }
+        }
+        bad[t] = b;
+    }
+    __syncthreads();
+    if (!any) return;
+    const int col = t & 63;
+    if (!bad[col] || c0 + col >= n) return;
+    for (int64_t r = t >> 6; r < nrows; r += 4) out[r * ld + c0 + col] = 0.0;
+}
+
 __global__ void zero_cols_kernel(double *out, int64_t nrows, int64_t ld, const int64_t *__restrict__ cols,
                                  int64_t ncols)
 {
@@ -448,17 +587,21 @@ __global__ void zero_cols_kernel(double *out, int64_t nrows, int64_t ld, const i
 // does not wait on a host round trip.  Radix select over order-preserving 64-bit
 // keys: six digit passes (11,11,11,11,11,9 bits, high to low) narrow the key
 // prefixes of the two order statistics numpy averages (k = n/2-1 and n/2 for even
-// n, n/2 twice for odd n).  Each pass is a histogram kernel (LDS bins, one global
-// atomic add per non-empty bin and workgroup) plus a one-workgroup select kernel
-// that scans the bins and extends the prefix.  The result is numpy's mean of the
-// two values, add.reduce order: (0 + ((0 + a) + b)) / 2; any NaN gives NaN.
+// n, n/2 twice for odd n).  Each pass is ONE histogram kernel (LDS bins, one global
+// atomic add per non-empty bin and workgroup): its workgroups first select the
+// previous pass's bin from that pass's global histogram themselves (every workgroup
+// computes the same prefix; workgroup 0 records it), and clear the buffer the next
+// pass will fill (three rotating buffers).  A one-workgroup final kernel selects the
+// last digit.  The result is numpy's mean of the two values, add.reduce order:
+// (0 + ((0 + a) + b)) / 2; any NaN gives NaN.  8 launches (was 14).
 constexpr int kMedBitsMax = 11;
 constexpr int kMedBins = 1 << kMedBitsMax;
 constexpr int kMedPasses = 6;
+constexpr int kMedBufs = 3;
 
 struct MedState {
-    uint64_t prefix[2];
-    int64_t k[2];
+    uint64_t prefix[kMedPasses + 1][2];  // key prefix of each target before pass p
+    int64_t k[kMedPasses + 1][2];        // its rank among the keys with that prefix
     uint32_t nan;
     uint32_t pad;
 };
@@ -482,24 +625,88 @@ __global__ void median_init_kernel(MedState *st, uint32_t *hist, int64_t n)
 {
     const int t = threadIdx.x;
     if (t == 0) {
-        st->prefix[0] = st->prefix[1] = 0;
-        st->k[0] = (n % 2 == 0) ? n / 2 - 1 : n / 2;
-        st->k[1] = n / 2;
+        st->prefix[0][0] = st->prefix[0][1] = 0;
+        st->k[0][0] = (n % 2 == 0) ? n / 2 - 1 : n / 2;
+        st->k[0][1] = n / 2;
         st->nan = 0;
     }
-    for (int i = t; i < 2 * kMedBins; i += blockDim.x) hist[i] = 0;
+    for (int i = t; i < kMedBufs * 2 * kMedBins; i += blockDim.x) hist[i] = 0;
+}
+
+// Block-wide selection (256 threads): the bin of ``hj`` holding rank k; thread t owns
+// bins [8t, 8t+8).  Returns (bin, rank inside the bin) to every thread.
+__device__ void med_select_block(const uint32_t *hj, int64_t k, uint32_t *scan, int64_t *res, int &bin,
+                                 int64_t &rem)
+{
+    const int t = threadIdx.x;
+    uint32_t c[8], sum = 0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        c[b] = hj[8 * t + b];
+        sum += c[b];
+    }
+    scan[t] = sum;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {
+        const uint32_t v = t >= off ? scan[t - off] : 0;
+        __syncthreads();
+        scan[t] += v;
+        __syncthreads();
+    }
+    const int64_t before = (int64_t)scan[t] - sum;
+    if (k >= before && k < before + (int64_t)sum) {
+        int64_t r = k - before;
+        int b = 0;
+        while (r >= (int64_t)c[b]) r -= c[b++];
+        res[0] = 8 * t + b;
+        res[1] = r;
+    }
+    __syncthreads();
+    bin = (int)res[0];
+    rem = res[1];
+    __syncthreads();
+}
+
+// Prefix and rank of both targets before pass ``pass`` (pass >= 1), from the previous
+// pass's histogram.
+__device__ void med_prefix(const MedState *st, const uint32_t *hist, int pass, uint32_t *scan, int64_t *res,
+                           uint64_t (&pfx)[2], int64_t (&kk)[2])
+{
+    const uint32_t *hp = hist + (size_t)((pass - 1) % kMedBufs) * 2 * kMedBins;
+    for (int j = 0; j < 2; ++j) {
+        int bin;
+        int64_t rem;
+        med_select_block(hp + j * kMedBins, st->k[pass - 1][j], scan, res, bin, rem);
+        pfx[j] = st->prefix[pass - 1][j] | ((uint64_t)bin << med_shift(pass - 1));
+        kk[j] = rem;
+    }
 }
 
 __global__ void __launch_bounds__(256)
 median_hist_kernel(const double *__restrict__ x, int64_t n, MedState *st, uint32_t *hist, int pass)
 {
     __shared__ uint32_t h[2][kMedBins];
+    __shared__ uint32_t scan[256];
+    __shared__ int64_t res[2];
+    uint64_t pfx[2] = {0, 0};
+    int64_t kk[2] = {st->k[0][0], st->k[0][1]};
+    if (pass > 0) {
+        med_prefix(st, hist, pass, scan, res, pfx, kk);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            st->prefix[pass][0] = pfx[0];
+            st->prefix[pass][1] = pfx[1];
+            st->k[pass][0] = kk[0];
+            st->k[pass][1] = kk[1];
+        }
+    }
+    // clear the buffer the NEXT pass accumulates into (nobody reads it during this pass)
+    uint32_t *nxt = hist + (size_t)((pass + 1) % kMedBufs) * 2 * kMedBins;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < 2 * kMedBins; i += gridDim.x * 256) nxt[i] = 0;
     for (int i = threadIdx.x; i < 2 * kMedBins; i += 256) (&h[0][0])[i] = 0;
     __syncthreads();
     const int shift = med_shift(pass), bits = med_bits(pass);
     const uint64_t dmask = (uint64_t(1) << bits) - 1;
     const int hs = shift + bits;  // bits above the digit must match the prefix
-    const uint64_t p0 = st->prefix[0], p1 = st->prefix[1];
     uint32_t nans = 0;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
         const double d = x[i];
@@ -509,66 +716,35 @@ median_hist_kernel(const double *__restrict__ x, int64_t n, MedState *st, uint32
         }
         const uint64_t k = order_key(d);
         const uint32_t dig = (uint32_t)((k >> shift) & dmask);
-        if (hs >= 64 || (k >> hs) == (p0 >> hs)) atomicAdd(&h[0][dig], 1u);
-        if (hs >= 64 || (k >> hs) == (p1 >> hs)) atomicAdd(&h[1][dig], 1u);
+        if (hs >= 64 || (k >> hs) == (pfx[0] >> hs)) atomicAdd(&h[0][dig], 1u);
+        if (hs >= 64 || (k >> hs) == (pfx[1] >> hs)) atomicAdd(&h[1][dig], 1u);
     }
     if (pass == 0 && nans) atomicAdd(&st->nan, nans);
     __syncthreads();
+    uint32_t *cur = hist + (size_t)(pass % kMedBufs) * 2 * kMedBins;
     for (int i = threadIdx.x; i < 2 * kMedBins; i += 256) {
         const uint32_t c = (&h[0][0])[i];
-        if (c) atomicAdd(&hist[i], c);
+        if (c) atomicAdd(&cur[i], c);
     }
 }
 
-// One workgroup: per target, thread t owns bins [8t, 8t+8); an exclusive scan of
-// the 256 partial counts finds the bin holding rank k; the bins are cleared for
-// the next pass.
-__global__ void __launch_bounds__(256) median_select_kernel(MedState *st, uint32_t *hist, int pass)
+// One workgroup: the last digit, then numpy's mean of the two order statistics.
+__global__ void __launch_bounds__(256) median_final_kernel(MedState *st, const uint32_t *hist, int64_t n,
+                                                           double *out)
 {
     __shared__ uint32_t scan[256];
-    const int t = threadIdx.x;
-    const int shift = med_shift(pass);
-    for (int j = 0; j < 2; ++j) {
-        uint32_t *hj = hist + j * kMedBins;
-        uint32_t c[8], sum = 0;
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            c[b] = hj[8 * t + b];
-            sum += c[b];
-        }
-        scan[t] = sum;
-        __syncthreads();
-        for (int off = 1; off < 256; off <<= 1) {
-            const uint32_t v = t >= off ? scan[t - off] : 0;
-            __syncthreads();
-            scan[t] += v;
-            __syncthreads();
-        }
-        const int64_t k = st->k[j];
-        const int64_t before = (int64_t)scan[t] - sum;
-        __syncthreads();
-        if (k >= before && k < before + (int64_t)sum) {
-            int64_t r = k - before;
-            int b = 0;
-            while (r >= (int64_t)c[b]) r -= c[b++];
-            st->prefix[j] |= (uint64_t)(8 * t + b) << shift;
-            st->k[j] = r;
-        }
-#pragma unroll
-        for (int b = 0; b < 8; ++b) hj[8 * t + b] = 0;
-        __syncthreads();
-    }
-}
-
-__global__ void median_final_kernel(const MedState *st, int64_t n, double *out)
-{
+    __shared__ int64_t res[2];
+    uint64_t pfx[2];
+    int64_t kk[2];
+    med_prefix(st, hist, kMedPasses, scan, res, pfx, kk);
+    if (threadIdx.x != 0) return;
     if (st->nan) {
         out[0] = __longlong_as_double(0x7ff8000000000000ll);
         return;
     }
-    const double a = key_value(st->prefix[0]);
+    const double a = key_value(pfx[0]);
     if (n % 2 == 0) {
-        const double b = key_value(st->prefix[1]);
+        const double b = key_value(pfx[1]);
         out[0] = (0.0 + ((0.0 + a) + b)) / 2.0;
     } else {
         out[0] = (0.0 + (0.0 + a)) / 1.0;
@@ -596,16 +772,29 @@ int row_sums_t(const void *x, int64_t nrows, int64_t n, int64_t ld, const void *
         // pair loads need 2-element alignment of every row (and of the scale vector)
         const bool pair = reinterpret_cast<uintptr_t>(x) % (2 * sizeof(Tin)) == 0 && ld % 2 == 0 &&
                           (MODE != 2 || reinterpret_cast<uintptr_t>(scale) % 16 == 0);
-        constexpr int R = MODE == 2 ? kScaleRows : 1;
-        const int64_t ngroups = (nrows + R - 1) / R;
-        PU_REQUIRE(ngroups * nfull < (int64_t(1) << 31), "pu_row_sums: too many blocks");
-        if (pair)
-            hipLaunchKernelGGL((rowsum_chunk_kernel<Tin, Ta, MODE, true, R>), dim3((unsigned)(ngroups * nfull)),
-                               dim3(256), 0, s, xp, ld, nrows, nfull, nblk_row, cp, scale, bs);
-        else
-            hipLaunchKernelGGL((rowsum_chunk_kernel<Tin, Ta, MODE, false, R>), dim3((unsigned)(ngroups * nfull)),
-                               dim3(256), 0, s, xp, ld, nrows, nfull, nblk_row, cp, scale, bs);
-        int rc = pu::launch_check("rowsum_chunk_kernel");
+        // MODE 2: R rows per workgroup share the scale pairs (PU_CLEAN_SCALE_ROWS: 4, 8, 16)
+        int rsel = kScaleRows;
+        if (const char *e = getenv("PU_CLEAN_SCALE_ROWS")) rsel = atoi(e);
+        auto go = [&](auto rc_) {
+            constexpr int R = MODE == 2 ? decltype(rc_)::value : 1;
+            const int64_t ngroups = (nrows + R - 1) / R;
+            PU_REQUIRE(ngroups * nfull < (int64_t(1) << 31), "pu_row_sums: too many blocks");
+            if (pair)
+                hipLaunchKernelGGL((rowsum_chunk_kernel<Tin, Ta, MODE, true, R>), dim3((unsigned)(ngroups * nfull)),
+                                   dim3(256), 0, s, xp, ld, nrows, nfull, nblk_row, cp, scale, bs);
+            else
+                hipLaunchKernelGGL((rowsum_chunk_kernel<Tin, Ta, MODE, false, R>),
+                                   dim3((unsigned)(ngroups * nfull)), dim3(256), 0, s, xp, ld, nrows, nfull,
+                                   nblk_row, cp, scale, bs);
+            return pu::launch_check("rowsum_chunk_kernel");
+        };
+        int rc;
+        if constexpr (MODE == 2) {
+            rc = rsel >= 16 ? go(std::integral_constant<int, 16>{})
+                            : rsel >= 8 ? go(std::integral_constant<int, 8>{}) : go(std::integral_constant<int, 4>{});
+        } else {
+            rc = go(std::integral_constant<int, 1>{});
+        }
         if (rc) return rc;
     }
     if (tail) {
@@ -652,7 +841,7 @@ int pick_vec(const void *p, int64_t ld, int vmax)
 // PU_CLEAN_VMAX overrides both (1, 2 or 4).
 int vec_max(size_t elem, int dflt)
 {
-    static const int env = [] {
+    const int env = [] {
         const char *e = getenv("PU_CLEAN_VMAX");
         return e ? atoi(e) : 0;
     }();
@@ -680,10 +869,17 @@ template <typename Tin>
 int col_means_t(const void *x, int64_t nrows, int64_t n, int64_t ld, const uint8_t *skip, double *out, hipStream_t s)
 {
     const int v = pick_vec<Tin>(x, ld, vec_max(sizeof(Tin), 4));
+    // bytes of rows in flight per lane and register buffer (PU_CLEAN_BATCH: 128 or 256)
+    int bb = kBatchBytes;
+    if (const char *e = getenv("PU_CLEAN_BATCH")) bb = atoi(e);
     return column_launches<Tin>(v, n, [&](auto vc, int64_t col0, int64_t ncols) {
         constexpr int V = decltype(vc)::value;
-        hipLaunchKernelGGL((colmean_kernel<Tin, V>), dim3(blocks_for(ncols / V, 256)), dim3(256), 0, s,
-                           reinterpret_cast<const Tin *>(x), nrows, col0, ncols, ld, skip, out);
+        if (bb >= 256)
+            hipLaunchKernelGGL((colmean_kernel<Tin, V, 256>), dim3(blocks_for(ncols / V, 256)), dim3(256), 0, s,
+                               reinterpret_cast<const Tin *>(x), nrows, col0, ncols, ld, skip, out);
+        else
+            hipLaunchKernelGGL((colmean_kernel<Tin, V, kBatchBytes>), dim3(blocks_for(ncols / V, 256)), dim3(256),
+                               0, s, reinterpret_cast<const Tin *>(x), nrows, col0, ncols, ld, skip, out);
     });
 }
 
@@ -691,7 +887,7 @@ int col_means_t(const void *x, int64_t nrows, int64_t n, int64_t ld, const uint8
 // 542 -> 481 us), off for float input (606 vs 623 us); PU_CLEAN_NT=0/1 overrides.
 bool nt_stores(size_t elem)
 {
-    static const int env = [] {
+    const int env = [] {
         const char *e = getenv("PU_CLEAN_NT");
         return e ? atoi(e) : -1;
     }();
@@ -818,7 +1014,29 @@ int pu_renorm_apply_zero_dm(const void *x, int dtype, int64_t nchan, int64_t n, 
     return renorm_apply_any(x, dtype, nchan, n, ld, factor, spec, bad, out, ld_out, col_means, ngood, stream);
 }
 
-size_t pu_median_workspace_bytes(void) { return sizeof(MedState) + 2 * kMedBins * sizeof(uint32_t); }
+size_t pu_cut_outliers_workspace_bytes(int64_t n)
+{
+    return 256 + (size_t)(n > 0 ? n : 0) * sizeof(double);
+}
+
+int pu_cut_outliers(const double *lc, int64_t n, double *out, int64_t nrows, int64_t ld_out, uint8_t *mask,
+                    void *ws, size_t ws_bytes, void *stream)
+{
+    PU_REQUIRE(lc && out && mask && n >= 64 && nrows > 0 && ld_out >= n, "pu_cut_outliers: bad arguments");
+    PU_REQUIRE(ws && ws_bytes >= pu_cut_outliers_workspace_bytes(n) && reinterpret_cast<uintptr_t>(ws) % 8 == 0,
+               "pu_cut_outliers: workspace too small or not 8-byte aligned");
+    hipStream_t s = pu::as_stream(stream);
+    OutlierState *st = reinterpret_cast<OutlierState *>(ws);
+    double *u = reinterpret_cast<double *>(reinterpret_cast<char *>(ws) + 256);
+    PU_TRY_HIP(hipMemsetAsync(st, 0, sizeof(OutlierState), s));
+    hipLaunchKernelGGL(outlier_window_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, lc, n, u, st);
+    hipLaunchKernelGGL(outlier_std_kernel, dim3(1), dim3(1024), 0, s, u, n, st);
+    hipLaunchKernelGGL(outlier_mask_zero_kernel, dim3(blocks_for(n, 64)), dim3(256), 0, s, u, n, st, mask, out,
+                       nrows, ld_out);
+    return pu::launch_check("outlier kernels");
+}
+
+size_t pu_median_workspace_bytes(void) { return sizeof(MedState) + kMedBufs * 2 * kMedBins * sizeof(uint32_t); }
 
 int pu_median(const double *x, int64_t n, double *out, void *ws, size_t ws_bytes, void *stream)
 {
@@ -829,12 +1047,11 @@ int pu_median(const double *x, int64_t n, double *out, void *ws, size_t ws_bytes
     MedState *st = reinterpret_cast<MedState *>(ws);
     uint32_t *hist = reinterpret_cast<uint32_t *>(st + 1);
     hipLaunchKernelGGL(median_init_kernel, dim3(1), dim3(256), 0, s, st, hist, n);
-    const unsigned grid = std::min<int64_t>(1024, std::max<int64_t>(1, (n + 255) / 256));
-    for (int p = 0; p < kMedPasses; ++p) {
+    // a few elements per thread: fewer workgroups to flush LDS bins to the global histogram
+    const unsigned grid = std::min<int64_t>(256, std::max<int64_t>(1, (n + 1023) / 1024));
+    for (int p = 0; p < kMedPasses; ++p)
         hipLaunchKernelGGL(median_hist_kernel, dim3(grid), dim3(256), 0, s, x, n, st, hist, p);
-        hipLaunchKernelGGL(median_select_kernel, dim3(1), dim3(256), 0, s, st, hist, p);
-    }
-    hipLaunchKernelGGL(median_final_kernel, dim3(1), dim3(1), 0, s, st, n, out);
+    hipLaunchKernelGGL(median_final_kernel, dim3(1), dim3(256), 0, s, st, hist, n, out);
     return pu::launch_check("median_kernels");
 }
 

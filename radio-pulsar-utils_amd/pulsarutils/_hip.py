@@ -49,6 +49,8 @@ SIGNATURES = {
     "pu_renorm_apply": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
     "pu_renorm_apply_zero_dm": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp]),
     "pu_zero_columns": (_i32, [_vp, _i64, _i64, _vp, _i64, _vp]),
+    "pu_cut_outliers_workspace_bytes": (_sz, [_i64]),
+    "pu_cut_outliers": (_i32, [_vp, _i64, _vp, _i64, _i64, _vp, _vp, _sz, _vp]),
     "pu_rebin_time": (_i32, [_vp, _i32, _i64, _i64, _i64, _i64, _vp, _vp]),
     "pu_rebin_chan": (_i32, [_vp, _i32, _i64, _i64, _i64, _i64, _vp, _vp]),
     "pu_roll_rows": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp]),

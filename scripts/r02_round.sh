@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round-2 GPU call: parity tests -> bench (C2 + clean + cpu baseline) -> pipeline timing.
+# Each GPU step has its own time limit; the script stops at the first failure.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+TAG=${TAG:-r02}
+if [ -z "$NOTEST" ]; then
+  timeout -k 10 1100 python -u -m pytest tests -v -m gpu -x --timeout 400 --timeout-method thread -p no:cacheprovider ${PYTEST_ARGS} > gpurun_out/${TAG}_tests.log 2>&1
+  rc=$?
+  echo "pytest rc=$rc" >> gpurun_out/${TAG}_tests.log
+  [ $rc -eq 0 ] || exit $rc
+fi
+if [ -z "$NOBENCH" ]; then
+  timeout -k 10 400 python -u bench.py --steps ${STEPS:-10} --warmup 2 ${BENCH_ARGS} > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || exit $?
+fi
+if [ -n "$PIPE" ]; then
+  timeout -k 10 400 python -u scripts/bench_pipeline.py --dtype u8 > gpurun_out/${TAG}_pipe_u8.json 2> gpurun_out/${TAG}_pipe_u8.err || exit $?
+  timeout -k 10 400 python -u scripts/bench_pipeline.py --dtype f32 --search f32 > gpurun_out/${TAG}_pipe_f32.json 2> gpurun_out/${TAG}_pipe_f32.err || exit $?
+fi
+if [ -n "$PROFILE" ]; then
+  export TMPDIR=/tmp
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/${TAG}_prof.log 2>&1 || exit $?
+fi
+exit 0
