@@ -114,6 +114,13 @@ int pu_plan_enable_timing(pu_plan *plan, int nslots);
  * launch order).  Returns the number written, or a negative PU_E* code. */
 int pu_plan_kernel_times(pu_plan *plan, float *ms, int n);
 
+/* Diagnostics: in the PU_STAMPS build (make stamps -> libpulsarutils_hip_stamps.so) the
+ * first call arms per-phase shader-clock stamps of the subband kernel and returns 0;
+ * later calls synchronise, write up to ``n`` (<= 8) summed wave-cycle totals {stage
+ * metadata, barrier A wait, build, barrier B wait, DMA issue, sum, epilogue, -} and
+ * reset them.  Returns 0 in the production build. */
+int pu_plan_stamps(pu_plan *plan, int64_t *out, int n);
+
 /* Introspection (tests / DESIGN.md): fills up to ``n`` of
  * {ndm, dm_tiles, time_tiles, trials_per_tile, time_tile, chans_per_step,
  *  row_stride, lds_bytes, acc_is_f64, max_spread, group, slots, stages,

@@ -39,7 +39,8 @@ namespace {
 
 constexpr int kBlock = 8192;   // numpy ufunc buffer size
 constexpr int kLeaf = 128;     // numpy PW_BLOCKSIZE
-constexpr int kScaleRows = 4;  // rows per workgroup of the scaled (MODE 2) row sums
+constexpr int kScaleRows = 16;  // rows per workgroup of the scaled (MODE 2) row sums
+                                // (C4 sweep: f32 191 vs 206 us at 4; u8 73 vs 86 us)
 
 template <typename Tin, typename Ta, int MODE>
 __device__ __forceinline__ Ta load_val(const Tin *row, int64_t t, Ta center, const double *scale)
@@ -870,7 +871,7 @@ int col_means_t(const void *x, int64_t nrows, int64_t n, int64_t ld, const uint8
 {
     const int v = pick_vec<Tin>(x, ld, vec_max(sizeof(Tin), 4));
     // bytes of rows in flight per lane and register buffer (PU_CLEAN_BATCH: 128 or 256)
-    int bb = kBatchBytes;
+    int bb = 256;  // C4 sweep (profiles/r02_clean/): f32 V=4 190 us vs 212 us at 128 B
     if (const char *e = getenv("PU_CLEAN_BATCH")) bb = atoi(e);
     return column_launches<Tin>(v, n, [&](auto vc, int64_t col0, int64_t ncols) {
         constexpr int V = decltype(vc)::value;
@@ -899,7 +900,8 @@ int renorm_apply_t(const void *x, int64_t nchan, int64_t n, int64_t ld, const do
                    const uint8_t *bad, double *out, int64_t ld_out, double *col_means, int64_t ngood_zdm,
                    hipStream_t s)
 {
-    const int vm = vec_max(sizeof(Tin), 1);
+    // C4 sweep (profiles/r02_clean/): f32 V=4 615 us (V=1 640), u8 V=2 + nt stores 480 us
+    const int vm = vec_max(sizeof(Tin), sizeof(Tin) == 4 ? 4 : sizeof(Tin) == 1 ? 2 : 1);
     const int v = std::min(pick_vec<Tin>(x, ld, vm), pick_vec<double>(out, ld_out, vm));
     const bool zdm = ngood_zdm >= 0;
     return column_launches<Tin>(v, n, [&](auto vc, int64_t col0, int64_t ncols) {

@@ -74,6 +74,20 @@ __device__ __forceinline__ T ld_uniform(const T *p)
     return *(const __attribute__((address_space(4))) T *)(p);
 }
 
+#ifdef PU_STAMPS
+// Diagnostic build only: a shader-clock stamp with the LDS queue drained, fenced
+// against scheduling (cdna_hip_programming.md §7, In-kernel stamps).  s_memtime is a
+// scalar-cache READ of the clock; the totals leave the kernel through vector atomics.
+__device__ __forceinline__ uint64_t stamp()
+{
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#endif
+
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
@@ -552,6 +566,8 @@ struct SubArgs {
     int32_t zero_len;       // floats of the zero row at LDS offset 0 (DMA mode, partial groups)
     int32_t lds_bytes;      // dynamic LDS size: a stage's raw rows end here
     int32_t skip;           // tuning ablation (PU_SUB_SKIP; results invalid): 1 build, 2 sum, 4 DMA
+    int32_t parts;          // build work items per slot (1..3)
+    void *stamps;           // diagnostic build (PU_STAMPS): 8 x u64 phase-cycle totals
 };
 
 // Counted LDS wait that also "defines" the J window registers it guards, so the adds
@@ -795,63 +811,88 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
         }
     };
 
-    // ---- build the stage's slots, one per wave at a time: R[i] (i < len) at copy 0 [i]
-    // and copy 1 [i - 1]; U chunks of 64 per pass, all G x U reads in flight
+    // ---- one build pass: chunks [i0, i0 + 64 UP) of a slot, written while < lim (whole
+    // chunks: lanes past len write row padding); reads of chunks past lim are clamped to
+    // the last written chunk (in range, results discarded).  All G x UP reads in flight.
+    auto build_pass = [&](auto upc, const meta_t &m, int gs, int i0, int lim) {
+        constexpr int UP = decltype(upc)::value;
+        float v[UP][G];
+        const int ilast = lim - 64;  // first element of the last chunk that is written
+        auto at = [&](int u) { return min(i0 + 64 * u, ilast) + lane; };
+        if (kDma || gs == G) {  // branch-free, all G x UP reads in flight (DMA mode: a
+                                // partial group's missing channels read the zero row)
+#pragma unroll
+            for (int u = 0; u < UP; ++u)
+#pragma unroll
+                for (int q = 0; q < G; ++q) v[u][q] = load(m, q, at(u));
+        } else {        // the last, partial group of a band
+#pragma unroll
+            for (int u = 0; u < UP; ++u)
+#pragma unroll
+                for (int q = 0; q < G; ++q) v[u][q] = q < gs ? load(m, q, at(u)) : 0.0f;
+        }
+        float r[UP];
+#pragma unroll
+        for (int u = 0; u < UP; ++u) {
+            r[u] = 0.0f;
+#pragma unroll
+            for (int q = 0; q < G; ++q) r[u] += v[u][q];
+        }
+        // all sums before the first (chunk-uniform) write branch: keeps every read
+        // of the pass in flight together
+#pragma unroll
+        for (int u = 0; u < UP; ++u) asm volatile("" : "+v"(r[u]));
+        // copy 0 at element i, copy 1 at element i - 1: lane-contiguous dwords, so
+        // ds_write_addtid_b32 (address = M0 + offset + 4 lane, no address VGPR):
+        // twice the LDS store rate of ds_write_b32 (MI355X_MICROARCH.md §LDS)
+        const uint32_t w0 = lds_base + (uint32_t)m[1] + 4u * (uint32_t)i0;
+        const uint32_t w1 = w0 + (uint32_t)copy_bytes - 4u;
+#pragma unroll
+        for (int u = 0; u < UP; ++u) {
+            if (i0 + 64 * u < lim) {
+                // M0 is saved and restored (the compiler owns it for the LDS-DMA);
+                // one wait state between an SALU write of M0 and an add-TID access
+                uint32_t saved;
+                asm volatile(
+                    "s_mov_b32 %0, m0\n\t"
+                    "s_mov_b32 m0, %2\n\t"
+                    "s_nop 0\n\t"
+                    "ds_write_addtid_b32 %1 offset:%4\n\t"
+                    "s_mov_b32 m0, %3\n\t"
+                    "s_nop 0\n\t"
+                    "ds_write_addtid_b32 %1 offset:%4\n\t"
+                    "s_mov_b32 m0, %0"
+                    : "=&s"(saved)
+                    : "v"(r[u]), "s"(w0), "s"(w1), "i"(256 * u)
+                    : "memory");
+            }
+        }
+    };
+
+    // ---- build the stage's slots: R[i] (i < len) at copy 0 [i] and copy 1 [i - 1] (copy
+    // 1's element -1 lands in copy 0's padding).  Work items are slot parts (a.parts per
+    // slot, PU_BUILD_PARTS): with ~20 slots per stage over 16 waves, whole slots leave
+    // most waves idle for half the phase; halves or thirds balance it.
+    constexpr int U2 = (U + 1) / 2, U3 = (U + 2) / 3;
     auto build = [&](const i32x4 st, const meta_t m0) {
-        for (int s = st.z + wave; s < st.w; s += W) {
-            const meta_t m = s == st.z + wave ? m0 : ld_uniform(reinterpret_cast<const meta_t *>(slots + (size_t)s * MS));
+        const int parts = a.parts;
+        const int nitems = (st.w - st.z) * parts;
+        for (int it = wave; it < nitems; it += W) {
+            const int s = st.z + it / parts, part = it - (it / parts) * parts;
+            const meta_t m = it == wave && parts == 1 ? m0
+                                                      : ld_uniform(reinterpret_cast<const meta_t *>(slots + (size_t)s * MS));
             const int len = m[0], gs = m[3];
-            // copy 1's element -1 lands in copy 0's padding
-            for (int i0 = 0; i0 < len; i0 += 64 * U) {
-                float v[U][G];
-                if (kDma || gs == G) {  // branch-free, all G x U reads in flight (DMA mode: a
-                                        // partial group's missing channels read the zero row)
-#pragma unroll
-                    for (int u = 0; u < U; ++u)
-#pragma unroll
-                        for (int q = 0; q < G; ++q) v[u][q] = load(m, q, i0 + 64 * u + lane);
-                } else {        // the last, partial group of a band
-#pragma unroll
-                    for (int u = 0; u < U; ++u)
-#pragma unroll
-                        for (int q = 0; q < G; ++q) v[u][q] = q < gs ? load(m, q, i0 + 64 * u + lane) : 0.0f;
-                }
-                float r[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    r[u] = 0.0f;
-#pragma unroll
-                    for (int q = 0; q < G; ++q) r[u] += v[u][q];
-                }
-                // all sums before the first (chunk-uniform) write branch: keeps every read
-                // of the pass in flight together
-#pragma unroll
-                for (int u = 0; u < U; ++u) asm volatile("" : "+v"(r[u]));
-                // copy 0 at element i, copy 1 at element i - 1: lane-contiguous dwords, so
-                // ds_write_addtid_b32 (address = M0 + offset + 4 lane, no address VGPR):
-                // twice the LDS store rate of ds_write_b32 (MI355X_MICROARCH.md §LDS)
-                const uint32_t w0 = lds_base + (uint32_t)m[1] + 4u * (uint32_t)i0;
-                const uint32_t w1 = w0 + (uint32_t)copy_bytes - 4u;
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    if (i0 + 64 * u < len) {  // whole chunks: lanes past len write row padding
-                        // M0 is saved and restored (the compiler owns it for the LDS-DMA);
-                        // one wait state between an SALU write of M0 and an add-TID access
-                        uint32_t saved;
-                        asm volatile(
-                            "s_mov_b32 %0, m0\n\t"
-                            "s_mov_b32 m0, %2\n\t"
-                            "s_nop 0\n\t"
-                            "ds_write_addtid_b32 %1 offset:%4\n\t"
-                            "s_mov_b32 m0, %3\n\t"
-                            "s_nop 0\n\t"
-                            "ds_write_addtid_b32 %1 offset:%4\n\t"
-                            "s_mov_b32 m0, %0"
-                            : "=&s"(saved)
-                            : "v"(r[u]), "s"(w0), "s"(w1), "i"(256 * u)
-                            : "memory");
-                    }
-                }
+            const int nch = (len + 63) >> 6;
+            const int per = (nch + parts - 1) / parts;
+            const int c0 = part * per, c1 = min(nch, c0 + per);
+            if (c0 >= c1) continue;
+            const int lim = 64 * c1;
+            if (parts == 1) {
+                for (int i0 = 0; i0 < len; i0 += 64 * U) build_pass(std::integral_constant<int, U>{}, m, gs, i0, lim);
+            } else if (parts == 2) {
+                for (int i0 = 64 * c0; i0 < lim; i0 += 64 * U2) build_pass(std::integral_constant<int, U2>{}, m, gs, i0, lim);
+            } else {
+                for (int i0 = 64 * c0; i0 < lim; i0 += 64 * U3) build_pass(std::integral_constant<int, U3>{}, m, gs, i0, lim);
             }
         }
     };
@@ -867,17 +908,29 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
     };
     i32x4 st = stage_at(0), st1 = stage_at(1);
     if constexpr (kDma) issue_raw(st, base_of(st));
+#ifdef PU_STAMPS
+    // diagnostic build only (make stamps): per-wave cycles per phase, summed over stages
+    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp = stamp(), tq;
+#define PU_PHASE(i) (tq = stamp(), ph[i] += tq - tp, tp = tq)
+#else
+#define PU_PHASE(i) ((void)0)
+#endif
     for (int k = 0; k < ns; ++k) {
         const i32x4 st2 = stage_at(k + 2);
         const int b1 = kDma ? base_of(st1) : 0;
         const meta_t m0 = meta_of(st);
         const rec_t rec0 = ld_uniform(recs + (size_t)st.x * W);
+        PU_PHASE(0);
         __syncthreads();  // raw rows of stage k landed (vmcnt); every wave left the slot area
+        PU_PHASE(1);
         if (!(a.skip & 1)) build(st, m0);
+        PU_PHASE(2);
         __syncthreads();  // slots built; every wave left the raw rows
+        PU_PHASE(3);
         if constexpr (kDma) {
             if (k + 1 < ns && !(a.skip & 4)) issue_raw(st1, b1);  // lands while this stage is summed
         }
+        PU_PHASE(4);
         if (active && !(a.skip & 2)) {
             const uint32_t sb = smem_addr + 8u * lane;  // window records: absolute LDS offsets
             rec_t rec = rec0;
@@ -887,11 +940,24 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
                 rec = next;
             }
         }
+        PU_PHASE(5);
         st = st1;
         st1 = st2;
     }
+#ifdef PU_STAMPS
+    if (active && !(a.skip & 8)) write_outputs<float, float, K, D, PLANE, STATS>(acc, o, first, slot0, cnt, t0, tt, lane);
+    PU_PHASE(6);
+    ph[7] = 1;
+    if (lane == 0 && a.stamps) {
+        for (int i = 0; i < 8; ++i) atomicAdd(reinterpret_cast<unsigned long long *>(a.stamps) + i,
+                                              (unsigned long long)ph[i]);
+    }
+#undef PU_PHASE
+#else
+#undef PU_PHASE
     if (!active || (a.skip & 8)) return;
     write_outputs<float, float, K, D, PLANE, STATS>(acc, o, first, slot0, cnt, t0, tt, lane);
+#endif
 }
 
 // One workgroup per trial: combine the per-time-tile partials in a fixed order
@@ -1026,6 +1092,7 @@ struct pu_plan {
     // each dispatch
     std::vector<hipEvent_t> ev_start, ev_stop;
     int64_t launches = 0;
+    uint64_t *d_stamps = nullptr;  // diagnostic build (PU_STAMPS): phase-cycle totals
 };
 
 namespace {
@@ -1083,6 +1150,9 @@ int launch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
     sa.zero_len = (int32_t)p->zero_len;
     sa.lds_bytes = (int32_t)p->lds_bytes;
     if (const char *env = getenv("PU_SUB_SKIP")) sa.skip = atoi(env);
+    sa.stamps = p->d_stamps;
+    sa.parts = 1;
+    if (const char *env = getenv("PU_BUILD_PARTS")) sa.parts = std::clamp(atoi(env), 1, 3);
     const dim3 grid((unsigned)((int64_t)p->ndt * a.ntt_run)), block(C::THREADS);
     auto go = [&](auto kern) {
         int rc = ensure_lds(kern, p->lds_bytes);
@@ -1163,6 +1233,7 @@ void free_plan(pu_plan *p)
     (void)hipFree(p->d_stages);
     (void)hipFree(p->d_slots);
     (void)hipFree(p->d_recs);
+    (void)hipFree(p->d_stamps);
     delete p;
 }
 
@@ -1773,6 +1844,28 @@ int pu_plan_enable_timing(pu_plan *p, int nslots)
     }
     p->launches = 0;
     return PU_OK;
+}
+
+int pu_plan_stamps(pu_plan *p, int64_t *out, int n)
+{
+    PU_REQUIRE(p != nullptr && out != nullptr, "pu_plan_stamps: bad arguments");
+#ifdef PU_STAMPS
+    if (!p->d_stamps) {
+        PU_TRY_HIP(hipMalloc((void **)&p->d_stamps, 8 * sizeof(uint64_t)));
+        PU_TRY_HIP(hipMemset(p->d_stamps, 0, 8 * sizeof(uint64_t)));
+        return 0;  // armed: the next launches accumulate
+    }
+    uint64_t h[8];
+    PU_TRY_HIP(hipDeviceSynchronize());
+    PU_TRY_HIP(hipMemcpy(h, p->d_stamps, sizeof h, hipMemcpyDeviceToHost));
+    PU_TRY_HIP(hipMemset(p->d_stamps, 0, 8 * sizeof(uint64_t)));
+    const int m = std::min(n, 8);
+    for (int i = 0; i < m; ++i) out[i] = (int64_t)h[i];
+    return m;
+#else
+    (void)n;
+    return 0;
+#endif
 }
 
 int pu_plan_kernel_times(pu_plan *p, float *ms, int n)

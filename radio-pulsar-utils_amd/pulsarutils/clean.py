@@ -133,6 +133,18 @@ def _gaussian_weights(sigma):
     return np.ascontiguousarray(_gaussian_kernel1d(sigma, 0, radius)[::-1]), radius
 
 
+_WEIGHTS = {}
+
+
+def _gaussian_weights_device(sigma, dev):
+    """scipy's gaussian_filter weights for ``sigma`` on ``dev``, uploaded once (cached)."""
+    key = (float(sigma), str(dev))
+    if key not in _WEIGHTS:
+        w, radius = _gaussian_weights(sigma)
+        _WEIGHTS[key] = (_hip.torch().from_numpy(w).to(dev), radius)
+    return _WEIGHTS[key]
+
+
 def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=False, out=None,
                        zero_dm=False):
     """renormalize_data on a device tensor; returns (float64 device tensor, bad_bins or None).
@@ -157,13 +169,14 @@ def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=
     if badchans_mask is None:
         badchans_mask = np.zeros(nchan, dtype=bool)
     bad_np = np.ascontiguousarray(np.asarray(badchans_mask, dtype=bool)).astype(np.uint8)
+    # host->device copies first: a pageable copy synchronises the stream, so none may
+    # sit between two kernels of the pass
     bad = t.from_numpy(bad_np).to(dev)
+    sigma = min(baseline_window, n // 100 * 2 + 1)
+    dw, radius = _gaussian_weights_device(sigma, dev)
     lc = t.empty(n, dtype=t.float64, device=dev)
     _hip.check(lib.pu_col_means(_hip.ptr(x), code, nchan, n, x.stride(0), _hip.ptr(bad), _hip.ptr(lc), s),
                "pu_col_means")
-    sigma = min(baseline_window, n // 100 * 2 + 1)
-    w, radius = _gaussian_weights(sigma)
-    dw = t.from_numpy(w).to(dev)
     smooth = t.empty(n, dtype=t.float64, device=dev)
     _hip.check(lib.pu_gaussian_filter1d(_hip.ptr(lc), n, _hip.ptr(dw), radius, _hip.ptr(smooth), s),
                "pu_gaussian_filter1d")

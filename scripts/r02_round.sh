@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 TAG=${TAG:-r02}
 if [ -z "$NOTEST" ]; then
-  timeout -k 10 1100 python -u -m pytest tests -v -m gpu -x --timeout 400 --timeout-method thread -p no:cacheprovider ${PYTEST_ARGS} > gpurun_out/${TAG}_tests.log 2>&1
+  timeout -k 10 1100 python -u -m pytest tests -v -m gpu -x --timeout 400 --timeout-method thread -p no:cacheprovider ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/${TAG}_tests.log 2>&1
   rc=$?
   echo "pytest rc=$rc" >> gpurun_out/${TAG}_tests.log
   [ $rc -eq 0 ] || exit $rc
@@ -17,6 +17,18 @@ fi
 if [ -n "$PIPE" ]; then
   timeout -k 10 400 python -u scripts/bench_pipeline.py --dtype u8 > gpurun_out/${TAG}_pipe_u8.json 2> gpurun_out/${TAG}_pipe_u8.err || exit $?
   timeout -k 10 400 python -u scripts/bench_pipeline.py --dtype f32 --search f32 > gpurun_out/${TAG}_pipe_f32.json 2> gpurun_out/${TAG}_pipe_f32.err || exit $?
+fi
+if [ -n "$SWEEP" ]; then
+  PU_SWEEP="$SWEEP" PU_ROUNDS=${ROUNDS:-3} timeout -k 10 600 python -u scripts/sweep.py ${SWEEP_CFG:-C2} > gpurun_out/${TAG}_sweep.log 2>&1 || exit $?
+fi
+if [ -n "$ABLATE" ]; then
+  for sk in $ABLATE; do
+    echo "skip=$sk" >> gpurun_out/${TAG}_ablate.log
+    PU_SUB_SKIP=$sk PU_ROUNDS=1 PU_SWEEP=${ABLATE_VARIANT:-4:160:0} timeout -k 10 200 python3 scripts/sweep.py C2 >> gpurun_out/${TAG}_ablate.log 2>&1 || exit $?
+  done
+fi
+if [ -n "$CLEANSWEEP" ]; then
+  timeout -k 10 400 python -u scripts/sweep_clean.py > gpurun_out/${TAG}_sweep_clean.jsonl 2>&1 || exit $?
 fi
 if [ -n "$PROFILE" ]; then
   export TMPDIR=/tmp
