@@ -567,6 +567,8 @@ struct SubArgs {
     int32_t lds_bytes;      // dynamic LDS size: a stage's raw rows end here
     int32_t skip;           // tuning ablation (PU_SUB_SKIP; results invalid): 1 build, 2 sum, 4 DMA
     int32_t parts;          // build work items per slot (1..3)
+    int32_t reuse;          // sum: skip window reads that repeat the previous trial's (PU_SUM_REUSE)
+    int32_t pad2;
     void *stamps;           // diagnostic build (PU_STAMPS): 8 x u64 phase-cycle totals
 };
 
@@ -657,6 +659,55 @@ __device__ __forceinline__ void group_trials(float (&acc)[C::D][C::K], const Rec
     }
 }
 
+// Same, reading only the windows that differ from the previous trial's.  Consecutive
+// plan trials often share a group's window (same relative-shift vector and the same
+// first-channel shift): at C2 5.3 of a wave's 8 windows per group are distinct.  A
+// repeated window is copied from the previous trial's registers (4 v_pk_mov-class moves
+// instead of 4 ds_read_b64); reads still run 3 trials ahead, and the counted wait before
+// a trial's adds covers exactly the reads issued after its own (0..3 windows: a
+// uniform branch picks the immediate).
+template <class C, typename RecT>
+__device__ __forceinline__ void group_trials_reuse(float (&acc)[C::D][C::K], const RecT rec, uint32_t base)
+{
+    constexpr int D = C::D, J = C::J;
+    double w[4][J];
+    bool dup[D];
+    dup[0] = false;
+#pragma unroll
+    for (int d = 1; d < D; ++d) dup[d] = rec[d] == rec[d - 1];
+#pragma unroll
+    for (int e = 0; e < 3 && e < D; ++e)
+        if (!dup[e]) issue_window<J>(w[e & 3], base + rec[e]);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        double(&wd)[J] = w[d & 3];
+        if (dup[d]) {  // before trial d + 3's read reuses buffer (d - 1) & 3
+#pragma unroll
+            for (int j = 0; j < J; ++j) wd[j] = w[(d + 3) & 3][j];
+        }
+        if (d + 3 < D && !dup[d + 3]) issue_window<J>(w[(d + 3) & 3], base + rec[d + 3]);
+        if (!dup[d]) {
+            int later = 0;  // windows issued after this trial's
+#pragma unroll
+            for (int e = d + 1; e <= d + 3 && e < D; ++e) later += dup[e] ? 0 : 1;
+            if (later == 3)
+                wait_window_n<J, 3 * J>(wd);
+            else if (later == 2)
+                wait_window_n<J, 2 * J>(wd);
+            else if (later == 1)
+                wait_window_n<J, J>(wd);
+            else
+                wait_window_n<J, 0>(wd);
+        }
+#pragma unroll
+        for (int k = 0; k < C::K; ++k) {
+            const uint64_t bits = __builtin_bit_cast(uint64_t, wd[k >> 1]);
+            acc[d][k] += __builtin_bit_cast(float, (uint32_t)((k & 1) ? (bits >> 32) : bits));
+        }
+        pin_accumulators(acc[d]);
+    }
+}
+
 // LDS-DMA of one channel-row window [start, start + cover) mod n (float32) into dst:
 // 1 KiB pieces (16 B/lane) while contiguous, per-lane modular dwords if it wraps.
 // Called by one wave; lands by the wave's next vmcnt(0) (the next barrier).
@@ -718,7 +769,7 @@ __device__ __forceinline__ void dma_row_u8(unsigned char *dst, const unsigned ch
 
 // DMA8: 8-bit rows staged by LDS-DMA as bytes (plans with n % 4 == 0); otherwise 8-bit
 // and float64 builds read global memory.
-template <class C, typename Tin, int G, bool PLANE, bool STATS, bool DMA8>
+template <class C, typename Tin, int G, bool PLANE, bool STATS, bool DMA8, bool REUSE = false>
 __global__ void __launch_bounds__(C::THREADS, 4)
 dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__restrict__ tile_stages,
                   const i32x4 *__restrict__ stages, const int32_t *__restrict__ slots,
@@ -869,31 +920,17 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
         }
     };
 
-    // ---- build the stage's slots: R[i] (i < len) at copy 0 [i] and copy 1 [i - 1] (copy
-    // 1's element -1 lands in copy 0's padding).  Work items are slot parts (a.parts per
-    // slot, PU_BUILD_PARTS): with ~20 slots per stage over 16 waves, whole slots leave
-    // most waves idle for half the phase; halves or thirds balance it.
-    constexpr int U2 = (U + 1) / 2, U3 = (U + 2) / 3;
+    // ---- build the stage's slots, one per wave at a time: R[i] (i < len) at copy 0 [i]
+    // and copy 1 [i - 1] (copy 1's element -1 lands in copy 0's padding).  (Splitting a
+    // slot over waves to balance the ~20 slots of a stage over 16 waves was measured
+    // slower: 22.1 / 25.6 vs 20.2 ms for halves / thirds - fewer reads in flight per
+    // pass, and the extra pass code spilled registers.)
     auto build = [&](const i32x4 st, const meta_t m0) {
-        const int parts = a.parts;
-        const int nitems = (st.w - st.z) * parts;
-        for (int it = wave; it < nitems; it += W) {
-            const int s = st.z + it / parts, part = it - (it / parts) * parts;
-            const meta_t m = it == wave && parts == 1 ? m0
-                                                      : ld_uniform(reinterpret_cast<const meta_t *>(slots + (size_t)s * MS));
+        for (int s = st.z + wave; s < st.w; s += W) {
+            const meta_t m = s == st.z + wave ? m0 : ld_uniform(reinterpret_cast<const meta_t *>(slots + (size_t)s * MS));
             const int len = m[0], gs = m[3];
-            const int nch = (len + 63) >> 6;
-            const int per = (nch + parts - 1) / parts;
-            const int c0 = part * per, c1 = min(nch, c0 + per);
-            if (c0 >= c1) continue;
-            const int lim = 64 * c1;
-            if (parts == 1) {
-                for (int i0 = 0; i0 < len; i0 += 64 * U) build_pass(std::integral_constant<int, U>{}, m, gs, i0, lim);
-            } else if (parts == 2) {
-                for (int i0 = 64 * c0; i0 < lim; i0 += 64 * U2) build_pass(std::integral_constant<int, U2>{}, m, gs, i0, lim);
-            } else {
-                for (int i0 = 64 * c0; i0 < lim; i0 += 64 * U3) build_pass(std::integral_constant<int, U3>{}, m, gs, i0, lim);
-            }
+            const int lim = (len + 63) & ~63;
+            for (int i0 = 0; i0 < len; i0 += 64 * U) build_pass(std::integral_constant<int, U>{}, m, gs, i0, lim);
         }
     };
 
@@ -936,7 +973,10 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
             rec_t rec = rec0;
             for (int g = st.x; g < st.y; ++g) {
                 const rec_t next = g + 1 < st.y ? ld_uniform(recs + (size_t)(g + 1) * W) : rec;
-                group_trials<C>(acc, rec, sb);
+                if constexpr (REUSE)
+                    group_trials_reuse<C>(acc, rec, sb);
+                else
+                    group_trials<C>(acc, rec, sb);
                 rec = next;
             }
         }
@@ -1151,6 +1191,8 @@ int launch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
     sa.lds_bytes = (int32_t)p->lds_bytes;
     if (const char *env = getenv("PU_SUB_SKIP")) sa.skip = atoi(env);
     sa.stamps = p->d_stamps;
+    sa.reuse = 0;
+    if (const char *env = getenv("PU_SUM_REUSE")) sa.reuse = atoi(env) != 0;
     sa.parts = 1;
     if (const char *env = getenv("PU_BUILD_PARTS")) sa.parts = std::clamp(atoi(env), 1, 3);
     const dim3 grid((unsigned)((int64_t)p->ndt * a.ntt_run)), block(C::THREADS);
@@ -1164,8 +1206,11 @@ int launch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
     if constexpr (std::is_same<Tin, uint8_t>::value) {
         if (p->dma8)
             return plane ? go(dedisp_sub_kernel<C, Tin, G, true, false, true>)
-                         : go(dedisp_sub_kernel<C, Tin, G, false, true, true>);
+                         : sa.reuse ? go(dedisp_sub_kernel<C, Tin, G, false, true, true, true>)
+                                    : go(dedisp_sub_kernel<C, Tin, G, false, true, true>);
     }
+    if constexpr (std::is_same<Tin, float>::value)
+        if (!plane && sa.reuse) return go(dedisp_sub_kernel<C, Tin, G, false, true, false, true>);
     return plane ? go(dedisp_sub_kernel<C, Tin, G, true, false, false>)
                  : go(dedisp_sub_kernel<C, Tin, G, false, true, false>);
 }
