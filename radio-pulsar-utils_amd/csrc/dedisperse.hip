@@ -567,7 +567,7 @@ struct SubArgs {
     int32_t lds_bytes;      // dynamic LDS size: a stage's raw rows end here
     int32_t skip;           // tuning ablation (PU_SUB_SKIP; results invalid): 1 build, 2 sum, 4 DMA
     int32_t parts;          // build work items per slot (1..3)
-    int32_t reuse;          // sum: skip window reads that repeat the previous trial's (PU_SUM_REUSE)
+    int32_t m0once;         // build: set M0 twice per pass instead of twice per chunk (PU_BUILD_M0)
     int32_t pad2;
     void *stamps;           // diagnostic build (PU_STAMPS): 8 x u64 phase-cycle totals
 };
@@ -659,55 +659,6 @@ __device__ __forceinline__ void group_trials(float (&acc)[C::D][C::K], const Rec
     }
 }
 
-// Same, reading only the windows that differ from the previous trial's.  Consecutive
-// plan trials often share a group's window (same relative-shift vector and the same
-// first-channel shift): at C2 5.3 of a wave's 8 windows per group are distinct.  A
-// repeated window is copied from the previous trial's registers (4 v_pk_mov-class moves
-// instead of 4 ds_read_b64); reads still run 3 trials ahead, and the counted wait before
-// a trial's adds covers exactly the reads issued after its own (0..3 windows: a
-// uniform branch picks the immediate).
-template <class C, typename RecT>
-__device__ __forceinline__ void group_trials_reuse(float (&acc)[C::D][C::K], const RecT rec, uint32_t base)
-{
-    constexpr int D = C::D, J = C::J;
-    double w[4][J];
-    bool dup[D];
-    dup[0] = false;
-#pragma unroll
-    for (int d = 1; d < D; ++d) dup[d] = rec[d] == rec[d - 1];
-#pragma unroll
-    for (int e = 0; e < 3 && e < D; ++e)
-        if (!dup[e]) issue_window<J>(w[e & 3], base + rec[e]);
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-        double(&wd)[J] = w[d & 3];
-        if (dup[d]) {  // before trial d + 3's read reuses buffer (d - 1) & 3
-#pragma unroll
-            for (int j = 0; j < J; ++j) wd[j] = w[(d + 3) & 3][j];
-        }
-        if (d + 3 < D && !dup[d + 3]) issue_window<J>(w[(d + 3) & 3], base + rec[d + 3]);
-        if (!dup[d]) {
-            int later = 0;  // windows issued after this trial's
-#pragma unroll
-            for (int e = d + 1; e <= d + 3 && e < D; ++e) later += dup[e] ? 0 : 1;
-            if (later == 3)
-                wait_window_n<J, 3 * J>(wd);
-            else if (later == 2)
-                wait_window_n<J, 2 * J>(wd);
-            else if (later == 1)
-                wait_window_n<J, J>(wd);
-            else
-                wait_window_n<J, 0>(wd);
-        }
-#pragma unroll
-        for (int k = 0; k < C::K; ++k) {
-            const uint64_t bits = __builtin_bit_cast(uint64_t, wd[k >> 1]);
-            acc[d][k] += __builtin_bit_cast(float, (uint32_t)((k & 1) ? (bits >> 32) : bits));
-        }
-        pin_accumulators(acc[d]);
-    }
-}
-
 // LDS-DMA of one channel-row window [start, start + cover) mod n (float32) into dst:
 // 1 KiB pieces (16 B/lane) while contiguous, per-lane modular dwords if it wraps.
 // Called by one wave; lands by the wave's next vmcnt(0) (the next barrier).
@@ -720,9 +671,11 @@ __device__ __forceinline__ void dma_row_f32(unsigned char *dst, const float *row
         for (; off + 1024 <= cover_bytes; off += 1024)
             __builtin_amdgcn_global_load_lds((const void *)(src + off + 16 * lane),
                                              (__attribute__((address_space(3))) void *)(dst + off), 16, 0, 0);
-        for (; off < cover_bytes; off += 256)
-            __builtin_amdgcn_global_load_lds((const void *)(src + off + 4 * lane),
-                                             (__attribute__((address_space(3))) void *)(dst + off), 4, 0, 0);
+        // the 256..768-byte tail as ONE 16-B/lane piece on the first rem/16 lanes (an
+        // LDS-DMA instruction costs ~100 issue cycles whatever its width)
+        if (off < cover_bytes && lane < (cover_bytes - off) / 16)
+            __builtin_amdgcn_global_load_lds((const void *)(src + off + 16 * lane),
+                                             (__attribute__((address_space(3))) void *)(dst + off), 16, 0, 0);
     } else {
         for (int off = 0; off < cover_bytes; off += 256) {
             int idx = start + (off >> 2) + lane;
@@ -749,9 +702,9 @@ __device__ __forceinline__ void dma_row_u8(unsigned char *dst, const unsigned ch
         for (; off + 1024 <= cover_bytes; off += 1024)
             __builtin_amdgcn_global_load_lds((const void *)(src + off + 16 * lane),
                                              (__attribute__((address_space(3))) void *)(dst + off), 16, 0, 0);
-        for (; off < cover_bytes; off += 256)
-            __builtin_amdgcn_global_load_lds((const void *)(src + off + 4 * lane),
-                                             (__attribute__((address_space(3))) void *)(dst + off), 4, 0, 0);
+        if (off < cover_bytes && lane < (cover_bytes - off) / 16)  // tail: one partial piece
+            __builtin_amdgcn_global_load_lds((const void *)(src + off + 16 * lane),
+                                             (__attribute__((address_space(3))) void *)(dst + off), 16, 0, 0);
     } else {
         const int nd = n >> 2;
         for (int off = 0; off < cover_bytes; off += 256) {
@@ -769,7 +722,7 @@ __device__ __forceinline__ void dma_row_u8(unsigned char *dst, const unsigned ch
 
 // DMA8: 8-bit rows staged by LDS-DMA as bytes (plans with n % 4 == 0); otherwise 8-bit
 // and float64 builds read global memory.
-template <class C, typename Tin, int G, bool PLANE, bool STATS, bool DMA8, bool REUSE = false>
+template <class C, typename Tin, int G, bool PLANE, bool STATS, bool DMA8>
 __global__ void __launch_bounds__(C::THREADS, 4)
 dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__restrict__ tile_stages,
                   const i32x4 *__restrict__ stages, const int32_t *__restrict__ slots,
@@ -898,6 +851,39 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
         // twice the LDS store rate of ds_write_b32 (MI355X_MICROARCH.md §LDS)
         const uint32_t w0 = lds_base + (uint32_t)m[1] + 4u * (uint32_t)i0;
         const uint32_t w1 = w0 + (uint32_t)copy_bytes - 4u;
+        if (a.m0once) {
+            // M0 set twice per pass (copy 0, then copy 1) instead of twice per chunk: the
+            // per-chunk save / set / nop / restore cost ~7 scalar issue slots per chunk
+            // on the CU's shared scalar unit.  M0 is saved and restored around the pass;
+            // nothing between these volatile statements uses it (no LDS-DMA or
+            // M0-relative instruction in the build).  When a copy spans whole passes
+            // (copy_bytes a multiple of 256 UP: C2's 2560 B at UP = 10) the chunks past
+            // len only write the slot's own padding, so the writes need no guards.
+            const bool whole = copy_bytes % (256 * UP) == 0;
+            uint32_t saved;
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0" : "=&s"(saved) : "s"(w0) : "memory");
+            if (whole) {
+#pragma unroll
+                for (int u = 0; u < UP; ++u)
+                    asm volatile("ds_write_addtid_b32 %0 offset:%1" : : "v"(r[u]), "i"(256 * u) : "memory");
+                asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(w1) : "memory");
+#pragma unroll
+                for (int u = 0; u < UP; ++u)
+                    asm volatile("ds_write_addtid_b32 %0 offset:%1" : : "v"(r[u]), "i"(256 * u) : "memory");
+            } else {
+#pragma unroll
+                for (int u = 0; u < UP; ++u)
+                    if (i0 + 64 * u < lim)
+                        asm volatile("ds_write_addtid_b32 %0 offset:%1" : : "v"(r[u]), "i"(256 * u) : "memory");
+                asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(w1) : "memory");
+#pragma unroll
+                for (int u = 0; u < UP; ++u)
+                    if (i0 + 64 * u < lim)
+                        asm volatile("ds_write_addtid_b32 %0 offset:%1" : : "v"(r[u]), "i"(256 * u) : "memory");
+            }
+            asm volatile("s_mov_b32 m0, %0" : : "s"(saved) : "memory");
+            return;
+        }
 #pragma unroll
         for (int u = 0; u < UP; ++u) {
             if (i0 + 64 * u < lim) {
@@ -973,10 +959,7 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
             rec_t rec = rec0;
             for (int g = st.x; g < st.y; ++g) {
                 const rec_t next = g + 1 < st.y ? ld_uniform(recs + (size_t)(g + 1) * W) : rec;
-                if constexpr (REUSE)
-                    group_trials_reuse<C>(acc, rec, sb);
-                else
-                    group_trials<C>(acc, rec, sb);
+                group_trials<C>(acc, rec, sb);
                 rec = next;
             }
         }
@@ -1191,8 +1174,8 @@ int launch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
     sa.lds_bytes = (int32_t)p->lds_bytes;
     if (const char *env = getenv("PU_SUB_SKIP")) sa.skip = atoi(env);
     sa.stamps = p->d_stamps;
-    sa.reuse = 0;
-    if (const char *env = getenv("PU_SUM_REUSE")) sa.reuse = atoi(env) != 0;
+    sa.m0once = 0;
+    if (const char *env = getenv("PU_BUILD_M0")) sa.m0once = atoi(env) != 0;
     sa.parts = 1;
     if (const char *env = getenv("PU_BUILD_PARTS")) sa.parts = std::clamp(atoi(env), 1, 3);
     const dim3 grid((unsigned)((int64_t)p->ndt * a.ntt_run)), block(C::THREADS);
@@ -1206,11 +1189,8 @@ int launch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
     if constexpr (std::is_same<Tin, uint8_t>::value) {
         if (p->dma8)
             return plane ? go(dedisp_sub_kernel<C, Tin, G, true, false, true>)
-                         : sa.reuse ? go(dedisp_sub_kernel<C, Tin, G, false, true, true, true>)
-                                    : go(dedisp_sub_kernel<C, Tin, G, false, true, true>);
+                         : go(dedisp_sub_kernel<C, Tin, G, false, true, true>);
     }
-    if constexpr (std::is_same<Tin, float>::value)
-        if (!plane && sa.reuse) return go(dedisp_sub_kernel<C, Tin, G, false, true, false, true>);
     return plane ? go(dedisp_sub_kernel<C, Tin, G, true, false, false>)
                  : go(dedisp_sub_kernel<C, Tin, G, false, true, false>);
 }
