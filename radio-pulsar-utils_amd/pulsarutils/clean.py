@@ -345,13 +345,50 @@ def search_by_chunks(fname, chunk_length=None, new_sample_time=None, tmin=0, dmm
     trial_DMs = None
     plan = None
     candidates = []
+    chunks = []
     for istart in range(0, nsamples, step // 2):
         chunk_size = min(step, nsamples - istart)
+        if istart * sample_time < tmin or chunk_size < step // 2:
+            continue
+        chunks.append((istart, chunk_size))
+    dev = t.device("cuda", t.cuda.current_device())
+    # Chunk k+1 is read from the memory-mapped file into a pinned buffer by a loader
+    # thread and copied to the device on a copy stream while chunk k is cleaned and
+    # searched; two pinned buffers alternate (a buffer is refilled only after its
+    # previous copy has completed).  With ``profile`` every step is synchronised instead.
+    overlap = profile is None and len(chunks) > 1
+    copy_stream = t.cuda.Stream(device=dev) if overlap else None
+    pinned = [None, None]
+    copied = [None, None]
+
+    def load(k):
+        istart, size = chunks[k]
+        view = fil._block_tc(istart, size)
+        b = k % 2
+        if copied[b] is not None:
+            copied[b].synchronize()
+        if pinned[b] is None or tuple(pinned[b].shape) != tuple(view.shape):
+            pinned[b] = t.empty(tuple(view.shape), dtype=t.from_numpy(np.empty(0, view.dtype)).dtype,
+                                pin_memory=True)
+        np.copyto(pinned[b].numpy(), view)
+        return pinned[b]
+
+    def upload(k, host):
+        with t.cuda.stream(copy_stream):
+            dst = host.to(dev, non_blocking=True)
+            ev = t.cuda.Event()
+            ev.record(copy_stream)
+        copied[k % 2] = ev
+        return dst, ev
+
+    pool = None
+    if overlap:
+        from concurrent.futures import ThreadPoolExecutor
+        pool = ThreadPoolExecutor(max_workers=1)
+        nxt = upload(0, load(0))
+        pending = pool.submit(load, 1)
+    for k, (istart, chunk_size) in enumerate(chunks):
         t0 = istart * sample_time
-        if t0 < tmin:
-            continue
-        if chunk_size < step // 2:
-            continue
         iend = istart + chunk_size
         marks = []
 
@@ -361,8 +398,13 @@ def search_by_chunks(fname, chunk_length=None, new_sample_time=None, tmin=0, dmm
                 marks.append((name, time.perf_counter()))
 
         mark("start")
-        tc = np.ascontiguousarray(fil._block_tc(istart, chunk_size))
-        src = t.from_numpy(tc).to(t.device("cuda", t.cuda.current_device()))
+        if overlap:
+            src, ev = nxt
+            t.cuda.current_stream(dev).wait_event(ev)
+            src.record_stream(t.cuda.current_stream(dev))
+        else:
+            tc = np.ascontiguousarray(fil._block_tc(istart, chunk_size))
+            src = t.from_numpy(tc).to(dev)
         mark("h2d")
         block = transpose_device(src)
         del src
@@ -377,6 +419,7 @@ def search_by_chunks(fname, chunk_length=None, new_sample_time=None, tmin=0, dmm
         if N > 1:
             array = _rebin_time_device(array, N)  # quick_resample of the float64 plane (clean.py:335-336)
         mark("rebin")
+        array64 = array  # the candidate pickles hold the float64 plane, as in the reference
         if search_dtype == "f32":
             array = array.to(t.float32)
         mark("cast")
@@ -387,6 +430,11 @@ def search_by_chunks(fname, chunk_length=None, new_sample_time=None, tmin=0, dmm
         (mx, sd, snr, win), plan = search_device(array, trial_DMs, nchan, start_freq, bandwidth, new_sample_time,
                                                  acc=acc, plan=plan)
         mark("search")
+        if overlap and k + 1 < len(chunks):
+            # the next chunk's copy overlaps this chunk's kernels (host waits on the loader)
+            nxt = upload(k + 1, pending.result())
+            if k + 2 < len(chunks):
+                pending = pool.submit(load, k + 2)
         if profile is not None:
             rec = {"istart": istart, "nsamples": chunk_size, "ndm": int(trial_DMs.size)}
             rec.update({name: (tt - marks[i][1]) * 1e3 for i, (name, tt) in enumerate(marks[1:])})
@@ -400,7 +448,7 @@ def search_by_chunks(fname, chunk_length=None, new_sample_time=None, tmin=0, dmm
             candidates.append(cand)
             if save_candidates:
                 info = PulseInfo()
-                info.allprofs = _host(array)
+                info.allprofs = _host(array64)
                 info.start_freq = start_freq
                 info.bandwidth = bandwidth
                 info.nbin = nbin
@@ -409,6 +457,9 @@ def search_by_chunks(fname, chunk_length=None, new_sample_time=None, tmin=0, dmm
                 info.pulse_freq = 1 / (info.nbin * new_sample_time)
                 with open(f'{fname_root}_{istart}-{iend}.pkl', 'wb') as fh:
                     pickle.dump(info, fh)
+        del array, array64
+    if pool is not None:
+        pool.shutdown(wait=True)
     return candidates
 
 
