@@ -566,8 +566,6 @@ struct SubArgs {
     int32_t zero_len;       // floats of the zero row at LDS offset 0 (DMA mode, partial groups)
     int32_t lds_bytes;      // dynamic LDS size: a stage's raw rows end here
     int32_t skip;           // tuning ablation (PU_SUB_SKIP; results invalid): 1 build, 2 sum, 4 DMA
-    int32_t parts;          // build work items per slot (1..3)
-    int32_t m0once;         // build: set M0 twice per pass instead of twice per chunk (PU_BUILD_M0)
     int32_t pad2;
     void *stamps;           // diagnostic build (PU_STAMPS): 8 x u64 phase-cycle totals
 };
@@ -851,59 +849,36 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
         // twice the LDS store rate of ds_write_b32 (MI355X_MICROARCH.md §LDS)
         const uint32_t w0 = lds_base + (uint32_t)m[1] + 4u * (uint32_t)i0;
         const uint32_t w1 = w0 + (uint32_t)copy_bytes - 4u;
-        if (a.m0once) {
-            // M0 set twice per pass (copy 0, then copy 1) instead of twice per chunk: the
-            // per-chunk save / set / nop / restore cost ~7 scalar issue slots per chunk
-            // on the CU's shared scalar unit.  M0 is saved and restored around the pass;
-            // nothing between these volatile statements uses it (no LDS-DMA or
-            // M0-relative instruction in the build).  When a copy spans whole passes
-            // (copy_bytes a multiple of 256 UP: C2's 2560 B at UP = 10) the chunks past
-            // len only write the slot's own padding, so the writes need no guards.
-            const bool whole = copy_bytes % (256 * UP) == 0;
-            uint32_t saved;
-            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0" : "=&s"(saved) : "s"(w0) : "memory");
-            if (whole) {
+        // M0 set twice per pass (copy 0, then copy 1), saved and restored around it (the
+        // compiler owns M0 for the LDS-DMA); nothing between these volatile statements uses
+        // it (no LDS-DMA or M0-relative instruction in the build).  Setting it around every
+        // chunk's two stores instead cost ~7 scalar issue slots per chunk on the CU's shared
+        // scalar unit (C2 19.97 -> 19.20 ms, C3 625 trials 156.5 -> 150.9 ms).  When a copy
+        // spans whole passes (copy_bytes a multiple of 256 UP: C2's 2560 B at UP = 10) the
+        // chunks past len only write the slot's own padding, so the stores need no guards.
+        const bool whole = copy_bytes % (256 * UP) == 0;
+        uint32_t saved;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0" : "=&s"(saved) : "s"(w0) : "memory");
+        if (whole) {
 #pragma unroll
-                for (int u = 0; u < UP; ++u)
+            for (int u = 0; u < UP; ++u)
+                asm volatile("ds_write_addtid_b32 %0 offset:%1" : : "v"(r[u]), "i"(256 * u) : "memory");
+            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(w1) : "memory");
+#pragma unroll
+            for (int u = 0; u < UP; ++u)
+                asm volatile("ds_write_addtid_b32 %0 offset:%1" : : "v"(r[u]), "i"(256 * u) : "memory");
+        } else {
+#pragma unroll
+            for (int u = 0; u < UP; ++u)
+                if (i0 + 64 * u < lim)
                     asm volatile("ds_write_addtid_b32 %0 offset:%1" : : "v"(r[u]), "i"(256 * u) : "memory");
-                asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(w1) : "memory");
+            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(w1) : "memory");
 #pragma unroll
-                for (int u = 0; u < UP; ++u)
+            for (int u = 0; u < UP; ++u)
+                if (i0 + 64 * u < lim)
                     asm volatile("ds_write_addtid_b32 %0 offset:%1" : : "v"(r[u]), "i"(256 * u) : "memory");
-            } else {
-#pragma unroll
-                for (int u = 0; u < UP; ++u)
-                    if (i0 + 64 * u < lim)
-                        asm volatile("ds_write_addtid_b32 %0 offset:%1" : : "v"(r[u]), "i"(256 * u) : "memory");
-                asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(w1) : "memory");
-#pragma unroll
-                for (int u = 0; u < UP; ++u)
-                    if (i0 + 64 * u < lim)
-                        asm volatile("ds_write_addtid_b32 %0 offset:%1" : : "v"(r[u]), "i"(256 * u) : "memory");
-            }
-            asm volatile("s_mov_b32 m0, %0" : : "s"(saved) : "memory");
-            return;
         }
-#pragma unroll
-        for (int u = 0; u < UP; ++u) {
-            if (i0 + 64 * u < lim) {
-                // M0 is saved and restored (the compiler owns it for the LDS-DMA);
-                // one wait state between an SALU write of M0 and an add-TID access
-                uint32_t saved;
-                asm volatile(
-                    "s_mov_b32 %0, m0\n\t"
-                    "s_mov_b32 m0, %2\n\t"
-                    "s_nop 0\n\t"
-                    "ds_write_addtid_b32 %1 offset:%4\n\t"
-                    "s_mov_b32 m0, %3\n\t"
-                    "s_nop 0\n\t"
-                    "ds_write_addtid_b32 %1 offset:%4\n\t"
-                    "s_mov_b32 m0, %0"
-                    : "=&s"(saved)
-                    : "v"(r[u]), "s"(w0), "s"(w1), "i"(256 * u)
-                    : "memory");
-            }
-        }
+        asm volatile("s_mov_b32 m0, %0" : : "s"(saved) : "memory");
     };
 
     // ---- build the stage's slots, one per wave at a time: R[i] (i < len) at copy 0 [i]
@@ -1174,10 +1149,6 @@ int launch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
     sa.lds_bytes = (int32_t)p->lds_bytes;
     if (const char *env = getenv("PU_SUB_SKIP")) sa.skip = atoi(env);
     sa.stamps = p->d_stamps;
-    sa.m0once = 0;
-    if (const char *env = getenv("PU_BUILD_M0")) sa.m0once = atoi(env) != 0;
-    sa.parts = 1;
-    if (const char *env = getenv("PU_BUILD_PARTS")) sa.parts = std::clamp(atoi(env), 1, 3);
     const dim3 grid((unsigned)((int64_t)p->ndt * a.ntt_run)), block(C::THREADS);
     auto go = [&](auto kern) {
         int rc = ensure_lds(kern, p->lds_bytes);

@@ -280,6 +280,18 @@ def dm_broadening(dm, freq, df):
     return 8300 * dm * df / freq**3
 
 
+_PINNED = []
+
+
+def _pinned_buffers(nbytes):
+    """Two page-locked host staging buffers of at least ``nbytes`` (kept across calls:
+    page-locking hundreds of MB costs tens of ms)."""
+    t = _hip.torch()
+    if not _PINNED or _PINNED[0].numel() < nbytes:
+        _PINNED[:] = [t.empty(int(nbytes), dtype=t.uint8, pin_memory=True) for _ in range(2)]
+    return _PINNED
+
+
 def search_by_chunks(fname, chunk_length=None, new_sample_time=None, tmin=0, dmmin=200, dmmax=800, surelybad=[],
                      save_candidates=True, snr_threshold=6, acc=None, search_dtype="f32", profile=None,
                      zero_dm=False):
@@ -358,8 +370,10 @@ def search_by_chunks(fname, chunk_length=None, new_sample_time=None, tmin=0, dmm
     # previous copy has completed).  With ``profile`` every step is synchronised instead.
     overlap = profile is None and len(chunks) > 1
     copy_stream = t.cuda.Stream(device=dev) if overlap else None
-    pinned = [None, None]
     copied = [None, None]
+    if overlap:
+        need = max(fil._block_tc(i, s).nbytes for i, s in chunks)
+        pinned = _pinned_buffers(need)
 
     def load(k):
         istart, size = chunks[k]
@@ -367,11 +381,9 @@ def search_by_chunks(fname, chunk_length=None, new_sample_time=None, tmin=0, dmm
         b = k % 2
         if copied[b] is not None:
             copied[b].synchronize()
-        if pinned[b] is None or tuple(pinned[b].shape) != tuple(view.shape):
-            pinned[b] = t.empty(tuple(view.shape), dtype=t.from_numpy(np.empty(0, view.dtype)).dtype,
-                                pin_memory=True)
-        np.copyto(pinned[b].numpy(), view)
-        return pinned[b]
+        host = pinned[b][:view.nbytes].view(t.from_numpy(np.empty(0, view.dtype)).dtype).view(view.shape)
+        np.copyto(host.numpy(), view)
+        return host
 
     def upload(k, host):
         with t.cuda.stream(copy_stream):

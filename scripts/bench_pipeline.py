@@ -67,12 +67,13 @@ def main():
             total = (time.perf_counter() - ta) * 1e3
         # the production mode: no per-step synchronisation, chunk k+1 read + copied while
         # chunk k is cleaned and searched
-        torch.cuda.synchronize()
-        ta = time.perf_counter()
-        clean.search_by_chunks(fname, chunk_length=chunk_length, dmmin=c4.dmmin, dmmax=c4.dmmax,
-                               save_candidates=False, snr_threshold=6, search_dtype=sd)
-        torch.cuda.synchronize()
-        overlapped = (time.perf_counter() - ta) * 1e3
+        for rep in range(2):  # the first call page-locks the staging buffers
+            torch.cuda.synchronize()
+            ta = time.perf_counter()
+            clean.search_by_chunks(fname, chunk_length=chunk_length, dmmin=c4.dmmin, dmmax=c4.dmmax,
+                                   save_candidates=False, snr_threshold=6, search_dtype=sd)
+            torch.cuda.synchronize()
+            overlapped = (time.perf_counter() - ta) * 1e3
         keys = ("h2d", "transpose", "clean", "rebin", "cast", "search")
         full = [p for p in prof if p["nsamples"] == 2 * half]
         mean = {k: float(np.mean([p[k] for p in full])) for k in keys}

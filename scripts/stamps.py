@@ -48,7 +48,7 @@ def main():
         return
     tot = float(out[:7].sum())
     rec = {"config": cfg.name, "plan": {k: plan.info[k] for k in ("group", "stages", "dm_tiles", "time_tiles")},
-           "env": {k: os.environ.get(k) for k in ("PU_BUILD_M0", "PU_SUB_SHAPE", "PU_GROUP") if os.environ.get(k)},
+           "env": {k: os.environ.get(k) for k in ("PU_SUB_SHAPE", "PU_GROUP") if os.environ.get(k)},
            "share": {p: round(float(out[i]) / tot, 4) for i, p in enumerate(PHASES)},
            "wave_cycles_per_launch": tot / launches}
     print(json.dumps(rec), flush=True)

@@ -1,9 +1,9 @@
 """Interleaved A/B of dedispersion plan variants in ONE process (guide §5.4 rule 24).
 
 Usage: python scripts/sweep.py [config]
-  env PU_SWEEP="G:KB[:shape[:parts]],..." selects (channel-group size, LDS budget KB,
-  subband workgroup shape 0 wide / 1 pair / 2 tall, build M0 once per pass 0/1) variants,
-  e.g. "1:64,4:160:0,4:80:1,4:160:0:1" (group 1 = channel mode).  PU_ROUNDS rounds.
+  env PU_SWEEP="G:KB[:shape],..." selects (channel-group size, LDS budget KB, subband
+  workgroup shape 0 wide / 1 pair / 2 tall) variants, e.g. "1:64,4:160:0,4:80:1" (group
+  1 = channel mode).  PU_ROUNDS rounds.
 Prints one line per (variant, round) and a median summary; the S/N of every trial
 is compared with the first variant's (float32 tolerance).
 """
@@ -38,7 +38,6 @@ res = {v: [] for v in plans}
 ref = None
 for r in range(rounds):
     for v, p in plans.items():
-        os.environ["PU_BUILD_M0"] = str(v[3] if len(v) > 3 else 0)
         p.enable_timing(3)
         for _ in range(3):
             out = p.search(x, workspace=ws)
