@@ -774,42 +774,24 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
     // ---- DMA mode: the channel rows of stage st into the raw area; base0 = this wave's
     // first row base (prefetched)
     const int32_t *base_t = base_tab + (size_t)dt * o.nchan;
-    // Work items are 1 KiB LDS-DMA pieces, dealt round-robin over the waves: ~19 rows of 3
-    // pieces per stage at C2 give every wave 3-4 pieces, where whole rows gave 3 of the 16
-    // waves two rows (6 pieces) - and the rest of the workgroup waited for them at the
-    // next barrier.  A row whose window wraps modulo n is moved whole (per-lane modular
-    // addresses) by the wave holding its piece 0.
-    const int cover_bytes_t = (tile.z * EB + 255) & ~255;
-    const int npiece = (cover_bytes_t + 1023) >> 10;  // pieces per row
     auto issue_raw = [&](const i32x4 st, int base0) {
         const int c0 = st.x * G;
         const int nc = min(st.y * G, o.nchan) - c0;
         // the stage's rows end at the top of LDS (the host packs stages so that they never
         // overlap the previous stage's slots, which are summed while these rows land)
         unsigned char *raw = smem + a.lds_bytes - ((nc * a.raw_stride * EB + 255) & ~255);
-        const int cover_bytes = cover_bytes_t;
-        const int nitems = nc * npiece;
-        for (int q = wave; q < nitems; q += W) {
-            const int ci = q / npiece, pc = q - ci * npiece;
+        const int cover_bytes = (tile.z * EB + 255) & ~255;
+        for (int ci = wave; ci < nc; ci += W) {
             const int c = c0 + ci;
-            int start = (q == wave ? base0 : ld_uniform(base_t + c)) + t0;
+            int start = (ci == wave ? base0 : ld_uniform(base_t + c)) + t0;
             if (start >= n) start -= n;
-            unsigned char *dst = raw + ci * a.raw_stride * EB;
-            const unsigned char *row = reinterpret_cast<const unsigned char *>(data) + (size_t)c * (size_t)o.ld * EB;
-            if (small_n || start + cover_bytes / EB > n) {  // wrapping window: whole row, piece-0 owner
-                if (pc == 0) {
-                    if constexpr (EB == 4)
-                        dma_row_f32(dst, reinterpret_cast<const float *>(row), start, cover_bytes, n, small_n, lane);
-                    else
-                        dma_row_u8(dst, row, start, cover_bytes, n, small_n, lane);
-                }
-                continue;
-            }
-            const int off = pc << 10;
-            const char *src = reinterpret_cast<const char *>(row) + (size_t)start * EB;
-            if (lane < min(1024, cover_bytes - off) / 16)  // the last piece may be partial
-                __builtin_amdgcn_global_load_lds((const void *)(src + off + 16 * lane),
-                                                 (__attribute__((address_space(3))) void *)(dst + off), 16, 0, 0);
+            if constexpr (EB == 4)
+                dma_row_f32(raw + ci * a.raw_stride * 4,
+                            reinterpret_cast<const float *>(data) + (size_t)c * (size_t)o.ld, start, cover_bytes, n,
+                            small_n, lane);
+            else
+                dma_row_u8(raw + ci * a.raw_stride, reinterpret_cast<const unsigned char *>(data) + (size_t)c * (size_t)o.ld,
+                           start, cover_bytes, n, small_n, lane);
         }
     };
 
@@ -918,7 +900,7 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
     // loads' latency overlaps the barrier waits instead of the phases.
     const int ns = ts.y;
     auto stage_at = [&](int k) { return ld_uniform(stages + ts.x + min(k, ns - 1)); };
-    auto base_of = [&](const i32x4 st) { return ld_uniform(base_t + min(st.x * G + wave / npiece, o.nchan - 1)); };
+    auto base_of = [&](const i32x4 st) { return ld_uniform(base_t + min(st.x * G + wave, o.nchan - 1)); };
     auto meta_of = [&](const i32x4 st) {
         return ld_uniform(reinterpret_cast<const meta_t *>(slots + (size_t)min(st.z + wave, st.w - 1) * MS));
     };

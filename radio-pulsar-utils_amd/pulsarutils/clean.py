@@ -280,18 +280,6 @@ def dm_broadening(dm, freq, df):
     return 8300 * dm * df / freq**3
 
 
-_PINNED = []
-
-
-def _pinned_buffers(nbytes):
-    """Two page-locked host staging buffers of at least ``nbytes`` (kept across calls:
-    page-locking hundreds of MB costs tens of ms)."""
-    t = _hip.torch()
-    if not _PINNED or _PINNED[0].numel() < nbytes:
-        _PINNED[:] = [t.empty(int(nbytes), dtype=t.uint8, pin_memory=True) for _ in range(2)]
-    return _PINNED
-
-
 def search_by_chunks(fname, chunk_length=None, new_sample_time=None, tmin=0, dmmin=200, dmmax=800, surelybad=[],
                      save_candidates=True, snr_threshold=6, acc=None, search_dtype="f32", profile=None,
                      zero_dm=False):
@@ -364,41 +352,27 @@ def search_by_chunks(fname, chunk_length=None, new_sample_time=None, tmin=0, dmm
             continue
         chunks.append((istart, chunk_size))
     dev = t.device("cuda", t.cuda.current_device())
-    # Chunk k+1 is read from the memory-mapped file into a pinned buffer by a loader
-    # thread and copied to the device on a copy stream while chunk k is cleaned and
-    # searched; two pinned buffers alternate (a buffer is refilled only after its
-    # previous copy has completed).  With ``profile`` every step is synchronised instead.
+    # Chunk k+1 is copied from the memory-mapped file to the device by a loader thread
+    # (a pageable H2D on a copy stream: the runtime's own staging, no extra host copy)
+    # while chunk k is cleaned and searched on the current stream.  With ``profile``
+    # every step is synchronised instead.
     overlap = profile is None and len(chunks) > 1
     copy_stream = t.cuda.Stream(device=dev) if overlap else None
-    copied = [None, None]
-    if overlap:
-        need = max(fil._block_tc(i, s).nbytes for i, s in chunks)
-        pinned = _pinned_buffers(need)
 
     def load(k):
         istart, size = chunks[k]
-        view = fil._block_tc(istart, size)
-        b = k % 2
-        if copied[b] is not None:
-            copied[b].synchronize()
-        host = pinned[b][:view.nbytes].view(t.from_numpy(np.empty(0, view.dtype)).dtype).view(view.shape)
-        np.copyto(host.numpy(), view)
-        return host
-
-    def upload(k, host):
-        with t.cuda.stream(copy_stream):
-            dst = host.to(dev, non_blocking=True)
+        tc = np.ascontiguousarray(fil._block_tc(istart, size))
+        with t.cuda.device(dev), t.cuda.stream(copy_stream):
+            dst = t.from_numpy(tc).to(dev)
             ev = t.cuda.Event()
             ev.record(copy_stream)
-        copied[k % 2] = ev
         return dst, ev
 
     pool = None
     if overlap:
         from concurrent.futures import ThreadPoolExecutor
         pool = ThreadPoolExecutor(max_workers=1)
-        nxt = upload(0, load(0))
-        pending = pool.submit(load, 1)
+        pending = pool.submit(load, 0)
     for k, (istart, chunk_size) in enumerate(chunks):
         t0 = istart * sample_time
         iend = istart + chunk_size
@@ -411,7 +385,9 @@ def search_by_chunks(fname, chunk_length=None, new_sample_time=None, tmin=0, dmm
 
         mark("start")
         if overlap:
-            src, ev = nxt
+            src, ev = pending.result()
+            if k + 1 < len(chunks):
+                pending = pool.submit(load, k + 1)
             t.cuda.current_stream(dev).wait_event(ev)
             src.record_stream(t.cuda.current_stream(dev))
         else:
@@ -442,11 +418,6 @@ def search_by_chunks(fname, chunk_length=None, new_sample_time=None, tmin=0, dmm
         (mx, sd, snr, win), plan = search_device(array, trial_DMs, nchan, start_freq, bandwidth, new_sample_time,
                                                  acc=acc, plan=plan)
         mark("search")
-        if overlap and k + 1 < len(chunks):
-            # the next chunk's copy overlaps this chunk's kernels (host waits on the loader)
-            nxt = upload(k + 1, pending.result())
-            if k + 2 < len(chunks):
-                pending = pool.submit(load, k + 2)
         if profile is not None:
             rec = {"istart": istart, "nsamples": chunk_size, "ndm": int(trial_DMs.size)}
             rec.update({name: (tt - marks[i][1]) * 1e3 for i, (name, tt) in enumerate(marks[1:])})

@@ -67,7 +67,7 @@ def main():
             total = (time.perf_counter() - ta) * 1e3
         # the production mode: no per-step synchronisation, chunk k+1 read + copied while
         # chunk k is cleaned and searched
-        for rep in range(2):  # the first call page-locks the staging buffers
+        for rep in range(2):  # the first call warms the loader thread and the allocator
             torch.cuda.synchronize()
             ta = time.perf_counter()
             clean.search_by_chunks(fname, chunk_length=chunk_length, dmmin=c4.dmmin, dmmax=c4.dmmax,
