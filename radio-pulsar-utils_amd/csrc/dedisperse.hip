@@ -472,7 +472,8 @@ dedisp_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const int32_
         const int c0 = k * a.ncc;
         const int nc = min(a.ncc, a.nchan - c0);
         const int b = kDma ? (k & 1) : 0;
-        __syncthreads();  // this wave's DMA landed (vmcnt) and every wave left the other buffer
+        if constexpr (kDma) asm volatile("s_waitcnt vmcnt(0)" : : : "memory");  // explicit (see dedisp_sub_kernel)
+        __syncthreads();  // this wave's DMA landed and every wave left the other buffer
         if constexpr (kDma) {
             if (k + 1 < nchunks) issue_dma(k + 1, b ^ 1);
         } else {
@@ -669,11 +670,11 @@ __device__ __forceinline__ void dma_row_f32(unsigned char *dst, const float *row
         for (; off + 1024 <= cover_bytes; off += 1024)
             __builtin_amdgcn_global_load_lds((const void *)(src + off + 16 * lane),
                                              (__attribute__((address_space(3))) void *)(dst + off), 16, 0, 0);
-        // the 256..768-byte tail as ONE 16-B/lane piece on the first rem/16 lanes (an
-        // LDS-DMA instruction costs ~100 issue cycles whatever its width)
-        if (off < cover_bytes && lane < (cover_bytes - off) / 16)
-            __builtin_amdgcn_global_load_lds((const void *)(src + off + 16 * lane),
-                                             (__attribute__((address_space(3))) void *)(dst + off), 16, 0, 0);
+        // the 256..768-byte tail in 256-B pieces (one partial 16-B/lane piece instead
+        // measured 0.15 ms slower at C2)
+        for (; off < cover_bytes; off += 256)
+            __builtin_amdgcn_global_load_lds((const void *)(src + off + 4 * lane),
+                                             (__attribute__((address_space(3))) void *)(dst + off), 4, 0, 0);
     } else {
         for (int off = 0; off < cover_bytes; off += 256) {
             int idx = start + (off >> 2) + lane;
@@ -771,19 +772,29 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
         for (int i = tid; i < a.zero_len; i += C::THREADS) zero[i] = 0.0f;
     }
 
-    // ---- DMA mode: the channel rows of stage st into the raw area; base0 = this wave's
-    // first row base (prefetched)
+    // ---- DMA mode: the channel rows of stage st into the raw area.  vb = this wave's row
+    // bases, lane k holding row wave + W k (one vector load per stage, issued a phase
+    // ahead: a scalar load per row put its latency in series with every row's DMA issue,
+    // ~10 % of the kernel's wave cycles at C2)
     const int32_t *base_t = base_tab + (size_t)dt * o.nchan;
-    auto issue_raw = [&](const i32x4 st, int base0) {
+    auto bases_of = [&](const i32x4 st) -> int {
+        const int c = st.x * G + wave + W * lane;
+        return c < min(st.y * G, o.nchan) ? base_t[c] : 0;
+    };
+    // this wave's rows of stage st: wave + W k for k < rows_of(st)
+    auto rows_of = [&](const i32x4 st) { return (min(st.y * G, o.nchan) - st.x * G - wave + W - 1) / W; };
+    // rows k in [kb, ke) of this wave
+    auto issue_raw = [&](const i32x4 st, int vb, int kb, int ke) {
         const int c0 = st.x * G;
         const int nc = min(st.y * G, o.nchan) - c0;
         // the stage's rows end at the top of LDS (the host packs stages so that they never
         // overlap the previous stage's slots, which are summed while these rows land)
         unsigned char *raw = smem + a.lds_bytes - ((nc * a.raw_stride * EB + 255) & ~255);
         const int cover_bytes = (tile.z * EB + 255) & ~255;
-        for (int ci = wave; ci < nc; ci += W) {
+        for (int k = kb; k < ke; ++k) {
+            const int ci = wave + W * k;
             const int c = c0 + ci;
-            int start = (ci == wave ? base0 : ld_uniform(base_t + c)) + t0;
+            int start = (k < 64 ? __builtin_amdgcn_readlane(vb, k) : ld_uniform(base_t + c)) + t0;
             if (start >= n) start -= n;
             if constexpr (EB == 4)
                 dma_row_f32(raw + ci * a.raw_stride * 4,
@@ -814,13 +825,15 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
     };
 
     // ---- one build pass: chunks [i0, i0 + 64 UP) of a slot, written while < lim (whole
-    // chunks: lanes past len write row padding); reads of chunks past lim are clamped to
-    // the last written chunk (in range, results discarded).  All G x UP reads in flight.
+    // chunks: lanes past len write row padding).  All G x UP reads in flight.  Reads of
+    // chunks past lim are not clamped: their results are discarded, and an LDS read past
+    // the allocation returns 0 (clamping them costs a VALU add per read - the reads then
+    // cannot fold 256 u into the ds_read offset field - and was measured 1.8 ms slower at
+    // C2, 20.2 vs 18.4 ms).
     auto build_pass = [&](auto upc, const meta_t &m, int gs, int i0, int lim) {
         constexpr int UP = decltype(upc)::value;
         float v[UP][G];
-        const int ilast = lim - 64;  // first element of the last chunk that is written
-        auto at = [&](int u) { return min(i0 + 64 * u, ilast) + lane; };
+        auto at = [&](int u) { return i0 + 64 * u + lane; };
         if (kDma || gs == G) {  // branch-free, all G x UP reads in flight (DMA mode: a
                                 // partial group's missing channels read the zero row)
 #pragma unroll
@@ -900,12 +913,11 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
     // loads' latency overlaps the barrier waits instead of the phases.
     const int ns = ts.y;
     auto stage_at = [&](int k) { return ld_uniform(stages + ts.x + min(k, ns - 1)); };
-    auto base_of = [&](const i32x4 st) { return ld_uniform(base_t + min(st.x * G + wave, o.nchan - 1)); };
     auto meta_of = [&](const i32x4 st) {
         return ld_uniform(reinterpret_cast<const meta_t *>(slots + (size_t)min(st.z + wave, st.w - 1) * MS));
     };
     i32x4 st = stage_at(0), st1 = stage_at(1);
-    if constexpr (kDma) issue_raw(st, base_of(st));
+    if constexpr (kDma) issue_raw(st, bases_of(st), 0, rows_of(st));
 #ifdef PU_STAMPS
     // diagnostic build only (make stamps): per-wave cycles per phase, summed over stages
     uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp = stamp(), tq;
@@ -915,18 +927,27 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
 #endif
     for (int k = 0; k < ns; ++k) {
         const i32x4 st2 = stage_at(k + 2);
-        const int b1 = kDma ? base_of(st1) : 0;
         const meta_t m0 = meta_of(st);
         const rec_t rec0 = ld_uniform(recs + (size_t)st.x * W);
         PU_PHASE(0);
-        __syncthreads();  // raw rows of stage k landed (vmcnt); every wave left the slot area
+        // This wave's LDS-DMA rows have landed before it arrives at the barrier.  Explicit:
+        // a workgroup-scope __syncthreads does not wait for vmcnt on gfx950, and the
+        // compiler's own LDS-DMA tracking puts its wait before this wave's first LDS read,
+        // after the barrier - too late for the other waves that read these rows.
+        asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
+        PU_PHASE(7);
+        __syncthreads();  // raw rows of stage k landed; every wave left the slot area
         PU_PHASE(1);
+        const int vb1 = kDma && k + 1 < ns ? bases_of(st1) : 0;  // lands during the build
         if (!(a.skip & 1)) build(st, m0);
         PU_PHASE(2);
         __syncthreads();  // slots built; every wave left the raw rows
         PU_PHASE(3);
         if constexpr (kDma) {
-            if (k + 1 < ns && !(a.skip & 4)) issue_raw(st1, b1);  // lands while this stage is summed
+            // the next stage's rows land while this stage is summed.  (Spreading these DMAs
+            // over the sum's groups instead was measured slower, 20.6 vs 18.5 ms at C2: the
+            // issue inside the sum breaks its read pipelining.)
+            if (k + 1 < ns && !(a.skip & 4)) issue_raw(st1, vb1, 0, rows_of(st1));
         }
         PU_PHASE(4);
         if (active && !(a.skip & 2)) {
@@ -945,7 +966,6 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
 #ifdef PU_STAMPS
     if (active && !(a.skip & 8)) write_outputs<float, float, K, D, PLANE, STATS>(acc, o, first, slot0, cnt, t0, tt, lane);
     PU_PHASE(6);
-    ph[7] = 1;
     if (lane == 0 && a.stamps) {
         for (int i = 0; i < 8; ++i) atomicAdd(reinterpret_cast<unsigned long long *>(a.stamps) + i,
                                               (unsigned long long)ph[i]);

@@ -22,7 +22,7 @@ from pulsarutils import _hip, synth  # noqa: E402
 from pulsarutils.configs import CONFIGS  # noqa: E402
 from pulsarutils.dedispersion import dedispersion_plan  # noqa: E402
 
-PHASES = ("metadata", "barrier_A_wait", "build", "barrier_B_wait", "dma_issue", "sum", "epilogue")
+PHASES = ("metadata", "barrier_A_wait", "build", "barrier_B_wait", "dma_issue", "sum", "epilogue", "dma_wait")
 
 
 def main():
@@ -46,7 +46,7 @@ def main():
     if m <= 0:
         print("not a stamps build", file=sys.stderr)
         return
-    tot = float(out[:7].sum())
+    tot = float(out[:8].sum())
     rec = {"config": cfg.name, "plan": {k: plan.info[k] for k in ("group", "stages", "dm_tiles", "time_tiles")},
            "env": {k: os.environ.get(k) for k in ("PU_SUB_SHAPE", "PU_GROUP") if os.environ.get(k)},
            "share": {p: round(float(out[i]) / tot, 4) for i, p in enumerate(PHASES)},
