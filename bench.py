@@ -151,7 +151,7 @@ def clean_bench(dev, steps):
                    "masks_alg_bytes": mask_bytes,
                    "masks_hbm_frac": round(mask_bytes / t_mask / 1e6 / HBM_PEAK_GBS, 4),
                    "bad_channels": int(bad.sum()), "variable_channels": int(var.sum()),
-                   "bad_bins": int(np.count_nonzero(bins))}
+                   "bad_bins": int(bins.sum().item())}
         del xd, out
         torch.cuda.empty_cache()
     res["roofline"] = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -358,7 +358,7 @@ __global__ void ratio_kernel(double num, const double *__restrict__ x, int64_t n
 // is the good channels' sum bit for bit); the second writes e - S[t]/ngood for good
 // channels and 0.0 for bad ones.  col_means (the cut_outliers series) is S[t]/nchan of
 // the normalised data BEFORE the subtraction, as without ZDM.
-template <typename Tin, int V, bool NT, bool ZDM>
+template <typename Tin, int V, bool NT, bool ZDM, int BB = kBatchBytes>
 __global__ void __launch_bounds__(256)
 apply_kernel(const Tin *__restrict__ x, int64_t nchan, int64_t col0, int64_t ncols, int64_t ld,
              const double *__restrict__ factor, const double *__restrict__ spec,
@@ -389,7 +389,7 @@ apply_kernel(const Tin *__restrict__ x, int64_t nchan, int64_t col0, int64_t nco
             const int rn = (int)(nchan - r0 < kRowChunk ? nchan - r0 : kRowChunk);
             stage(r0, rn);
             if (!active) continue;
-            walk_rows<Tin, V>(x + r0 * ld + c, ld, rn, [&](int i, const Vec<Tin, V> &v) {
+            auto sum_fn = [&](int i, const Vec<Tin, V> &v) {
                 const double mu = mus[i];
                 const bool b = bads[i] != 0;
 #pragma unroll
@@ -398,7 +398,8 @@ apply_kernel(const Tin *__restrict__ x, int64_t nchan, int64_t col0, int64_t nco
                     e = (e - mu) / mu;
                     acc[j] += b ? 0.0 : e;
                 }
-            });
+            };
+            walk_rows<Tin, V, decltype(sum_fn) &, BB>(x + r0 * ld + c, ld, rn, sum_fn);
         }
 #pragma unroll
         for (int j = 0; j < V; ++j) zsub[j] = ngood > 0 ? acc[j] / static_cast<double>(ngood) : 0.0;
@@ -408,7 +409,7 @@ apply_kernel(const Tin *__restrict__ x, int64_t nchan, int64_t col0, int64_t nco
         stage(r0, rn);
         if (!active) continue;
         double *o = out + r0 * ld_out + c;
-        walk_rows<Tin, V>(x + r0 * ld + c, ld, rn, [&](int i, const Vec<Tin, V> &v) {
+        auto apply_fn = [&](int i, const Vec<Tin, V> &v) {
             const double mu = mus[i];
             const bool b = bads[i] != 0;
             Vec<double, V> res;
@@ -429,7 +430,8 @@ apply_kernel(const Tin *__restrict__ x, int64_t nchan, int64_t col0, int64_t nco
             } else {
                 *reinterpret_cast<Vec<double, V> *>(o + (int64_t)i * ld_out) = res;
             }
-        });
+        };
+        walk_rows<Tin, V, decltype(apply_fn) &, BB>(x + r0 * ld + c, ld, rn, apply_fn);
     }
     if (!active || !col_means) return;
 #pragma unroll
@@ -468,7 +470,8 @@ __device__ __forceinline__ int64_t reflect_small(int64_t i, int64_t n)
 }
 
 __global__ void __launch_bounds__(256)
-outlier_window_kernel(const double *__restrict__ lc, int64_t n, double *__restrict__ u, OutlierState *st)
+outlier_window_kernel(const double *__restrict__ lc, int64_t n, double *__restrict__ u, double *__restrict__ u16,
+                      OutlierState *st)
 {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     double s = 0.0, a = 0.0;
@@ -476,6 +479,7 @@ outlier_window_kernel(const double *__restrict__ lc, int64_t n, double *__restri
     if (i < n) {
         for (int j = -8; j < 8; ++j) s += lc[(i + j >= 0 && i + j < n) ? i + j : reflect_small(i + j, n)];
         u[i] = s / 16.0;
+        if ((i & 15) == 0) u16[i >> 4] = s / 16.0;  // u[::16], compact for the std pass
         const double x = lc[i];
         nan = x != x;
         a = fabs(x);
@@ -497,35 +501,38 @@ outlier_window_kernel(const double *__restrict__ lc, int64_t n, double *__restri
     }
 }
 
-// One workgroup: sd = std(u[::16]) (two passes), thresholds and certification margins.
-__global__ void __launch_bounds__(1024) outlier_std_kernel(const double *__restrict__ u, int64_t n, OutlierState *st)
+// Block-wide sum (1024 threads): wave sums by xor shuffles, then the 16 wave totals.
+__device__ __forceinline__ double block_sum_1024(double v, double *red)
 {
-    __shared__ double red[1024];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    const int t = threadIdx.x;
+    __syncthreads();  // red is reused between calls
+    if ((t & 63) == 0) red[t >> 6] = v;
+    __syncthreads();
+    double tot = 0.0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) tot += red[w];
+    return tot;
+}
+
+// One workgroup: sd = std(u[::16]) (two passes over the compact copy), thresholds and
+// certification margins.  (Any summation order: the margins bound the difference.)
+__global__ void __launch_bounds__(1024) outlier_std_kernel(const double *__restrict__ u16, int64_t n, OutlierState *st)
+{
+    __shared__ double red[16];
     const int t = threadIdx.x;
     const int64_t m = (n + 15) / 16;
     double s = 0.0;
-    for (int64_t k = t; k < m; k += 1024) s += u[16 * k];
-    red[t] = s;
-    __syncthreads();
-    for (int w = 512; w > 0; w >>= 1) {
-        if (t < w) red[t] += red[t + w];
-        __syncthreads();
-    }
-    const double mean = red[0] / (double)m;
-    __syncthreads();
+    for (int64_t k = t; k < m; k += 1024) s += u16[k];
+    const double mean = block_sum_1024(s, red) / (double)m;
     s = 0.0;
     for (int64_t k = t; k < m; k += 1024) {
-        const double d = u[16 * k] - mean;
+        const double d = u16[k] - mean;
         s += d * d;
     }
-    red[t] = s;
-    __syncthreads();
-    for (int w = 512; w > 0; w >>= 1) {
-        if (t < w) red[t] += red[t + w];
-        __syncthreads();
-    }
+    const double ss = block_sum_1024(s, red);
     if (t == 0) {
-        const double sd = sqrt(red[0] / (double)m);
+        const double sd = sqrt(ss / (double)m);
         const double L = __longlong_as_double((long long)st->lbits);
         const double E = ((double)(2 * n + 64) * 0x1p-53) * L + 1e-300;  // |u - v| bound
         const double Es = E + 1e-12 * sd;                                  // |std(u) - std(v)| bound
@@ -912,10 +919,21 @@ int renorm_apply_t(const void *x, int64_t nchan, int64_t n, int64_t ld, const do
                                ld_out, col_means, ngood_zdm);
         };
         const bool nt = nt_stores(sizeof(Tin));
+        // bytes of rows in flight per lane and register buffer (PU_APPLY_BATCH)
+        int bb = kBatchBytes;
+        if (const char *e = getenv("PU_APPLY_BATCH")) bb = atoi(e);
+        auto pick = [&](auto ntc, auto zc) {
+            constexpr bool NT = decltype(ntc)::value, Z = decltype(zc)::value;
+            if (bb >= 512) go(apply_kernel<Tin, V, NT, Z, 512>);
+            else if (bb >= 256) go(apply_kernel<Tin, V, NT, Z, 256>);
+            else go(apply_kernel<Tin, V, NT, Z, kBatchBytes>);
+        };
+        using T_ = std::true_type;
+        using F_ = std::false_type;
         if (zdm)
-            nt ? go(apply_kernel<Tin, V, true, true>) : go(apply_kernel<Tin, V, false, true>);
+            nt ? pick(T_{}, T_{}) : pick(F_{}, T_{});
         else
-            nt ? go(apply_kernel<Tin, V, true, false>) : go(apply_kernel<Tin, V, false, false>);
+            nt ? pick(T_{}, F_{}) : pick(F_{}, F_{});
     });
 }
 
@@ -1018,7 +1036,8 @@ int pu_renorm_apply_zero_dm(const void *x, int dtype, int64_t nchan, int64_t n, 
 
 size_t pu_cut_outliers_workspace_bytes(int64_t n)
 {
-    return 256 + (size_t)(n > 0 ? n : 0) * sizeof(double);
+    const size_t m = (size_t)(n > 0 ? n : 0);
+    return 256 + (m + (m + 15) / 16) * sizeof(double);  // state | window means | every 16th
 }
 
 int pu_cut_outliers(const double *lc, int64_t n, double *out, int64_t nrows, int64_t ld_out, uint8_t *mask,
@@ -1030,9 +1049,10 @@ int pu_cut_outliers(const double *lc, int64_t n, double *out, int64_t nrows, int
     hipStream_t s = pu::as_stream(stream);
     OutlierState *st = reinterpret_cast<OutlierState *>(ws);
     double *u = reinterpret_cast<double *>(reinterpret_cast<char *>(ws) + 256);
+    double *u16 = u + n;
     PU_TRY_HIP(hipMemsetAsync(st, 0, sizeof(OutlierState), s));
-    hipLaunchKernelGGL(outlier_window_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, lc, n, u, st);
-    hipLaunchKernelGGL(outlier_std_kernel, dim3(1), dim3(1024), 0, s, u, n, st);
+    hipLaunchKernelGGL(outlier_window_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, lc, n, u, u16, st);
+    hipLaunchKernelGGL(outlier_std_kernel, dim3(1), dim3(1024), 0, s, u16, n, st);
     hipLaunchKernelGGL(outlier_mask_zero_kernel, dim3(blocks_for(n, 64)), dim3(256), 0, s, u, n, st, mask, out,
                        nrows, ld_out);
     return pu::launch_check("outlier kernels");

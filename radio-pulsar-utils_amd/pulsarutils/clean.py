@@ -147,7 +147,9 @@ def _gaussian_weights_device(sigma, dev):
 
 def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=False, out=None,
                        zero_dm=False):
-    """renormalize_data on a device tensor; returns (float64 device tensor, bad_bins or None).
+    """renormalize_data on a device tensor; returns (float64 device tensor, bad_bins or None),
+    bad_bins a boolean device tensor (the cut_outliers time-bin mask; not copied to the
+    host: renormalize_data discards it, as the reference does).
 
     Passes (clean.py:73-105): zero-DM light curve over good channels (column means,
     rows in order) -> gaussian_filter (GPU, scipy's order) -> median (GPU radix
@@ -206,7 +208,7 @@ def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=
                                        _hip.ptr(ws), ws.numel(), s), "pu_cut_outliers")
         flag = int(ws[:4].view(t.int32).item())
         if flag == 0:
-            return out, _host(mask).astype(bool)
+            return out, mask.view(t.bool)
         # ambiguous (a window mean within rounding distance of a threshold) or NaN: redo
         # the apply pass (the plane may already have zeroed columns) and run scipy's own
         # running-sum filter on the host, as the reference does
@@ -230,6 +232,7 @@ def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=
             dcols = t.from_numpy(cols).to(dev)
             _hip.check(lib.pu_zero_columns(_hip.ptr(out), nchan, out.stride(0), _hip.ptr(dcols), cols.size, s),
                        "pu_zero_columns")
+        bad_bins = t.from_numpy(bad_bins).to(dev)
     return out, bad_bins
 
 

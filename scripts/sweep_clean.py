@@ -47,7 +47,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dtype", default="f32,u8")
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--kernels", default="col_means,row_sums_scaled,apply,median,renormalize_device")
     args = ap.parse_args()
+    want = set(args.kernels.split(","))
     lib = _hip.lib()
     cfg = CONFIGS["C4"]
     for dt in args.dtype.split(","):
@@ -70,29 +72,40 @@ def main():
                               "GBps": round(nbytes / ms / 1e6, 1), "hbm_frac": round(nbytes / ms / 1e6 / HBM, 3)}),
                   flush=True)
 
-        for vmax in (1, 2, 4):
+        for vmax in ((1, 2, 4) if "col_means" in want else ()):
             for batch in (128, 256):
                 setenv(PU_CLEAN_VMAX=vmax, PU_CLEAN_BATCH=batch)
                 ms = timed(lambda: lib.pu_col_means(_hip.ptr(x), code, nchan, n, x.stride(0), _hip.ptr(bad),
                                                     _hip.ptr(lc), s), args.steps)
                 rec("col_means", {"vmax": vmax, "batch": batch}, ms, plane)
         setenv(PU_CLEAN_VMAX=None, PU_CLEAN_BATCH=None)
-        for rows in (4, 8, 16):
+        for rows in ((4, 8, 16) if "row_sums_scaled" in want else ()):
             setenv(PU_CLEAN_SCALE_ROWS=rows)
             ms = timed(lambda: clean._row_sums(x, 2, scale=factor, divisor=n), args.steps)
             rec("row_sums_scaled", {"rows": rows}, ms, plane)
         setenv(PU_CLEAN_SCALE_ROWS=None)
-        for vmax in (1, 2, 4):
+        for vmax in ((1, 2, 4) if "apply" in want else ()):
             for nt in (0, 1):
-                setenv(PU_CLEAN_VMAX=vmax, PU_CLEAN_NT=nt)
-                ms = timed(lambda: lib.pu_renorm_apply(_hip.ptr(x), code, nchan, n, x.stride(0), _hip.ptr(factor),
-                                                       _hip.ptr(spec), _hip.ptr(bad), _hip.ptr(out), out.stride(0),
-                                                       _hip.ptr(col), s), args.steps)
-                rec("apply", {"vmax": vmax, "nt": nt}, ms, plane + nchan * n * 8)
-        setenv(PU_CLEAN_VMAX=None, PU_CLEAN_NT=None)
-        ms = timed(lambda: clean.median_device(lc), args.steps)
-        rec("median", {}, ms, n * 8)
-        for cut in (False, True):
+                for batch in (128, 256, 512):
+                    setenv(PU_CLEAN_VMAX=vmax, PU_CLEAN_NT=nt, PU_APPLY_BATCH=batch)
+                    ms = timed(lambda: lib.pu_renorm_apply(_hip.ptr(x), code, nchan, n, x.stride(0),
+                                                           _hip.ptr(factor), _hip.ptr(spec), _hip.ptr(bad),
+                                                           _hip.ptr(out), out.stride(0), _hip.ptr(col), s), args.steps)
+                    rec("apply", {"vmax": vmax, "nt": nt, "batch": batch}, ms, plane + nchan * n * 8)
+        setenv(PU_CLEAN_VMAX=None, PU_CLEAN_NT=None, PU_APPLY_BATCH=None)
+        if "ceiling" in want:
+            # the same traffic (read the plane, write it as float64) by torch's own
+            # elementwise cast kernel: the achievable rate for this read/write mix
+            ms = timed(lambda: out.copy_(x), args.steps)
+            rec("ceiling_cast_copy", {}, ms, plane + nchan * n * 8)
+            y = torch.empty_like(out)
+            ms = timed(lambda: y.copy_(out), args.steps)
+            rec("ceiling_f64_copy", {}, ms, 2 * nchan * n * 8)
+            del y
+        if "median" in want:
+            ms = timed(lambda: clean.median_device(lc), args.steps)
+            rec("median", {}, ms, n * 8)
+        for cut in ((False, True) if "renormalize_device" in want else ()):
             ms = timed(lambda: clean.renormalize_device(x, badchans_mask=bad_np, cut_outliers=cut, out=out),
                        args.steps)
             rec("renormalize_device", {"cut_outliers": cut}, ms, 3 * plane + nchan * n * 8)

@@ -43,7 +43,7 @@ def check_case(golden, tag, x):
             pytest.fail(f"{key}: {len(diff)} elements differ, first {diff[:5].tolist()}")
         if cut:
             expect = arrays[key + "_badbins"]
-            np.testing.assert_array_equal(np.nonzero(bins)[0], expect)
+            np.testing.assert_array_equal(np.nonzero(bins.cpu().numpy())[0], expect)
         del out
         torch.cuda.empty_cache()
 
@@ -120,7 +120,7 @@ def test_zero_dm_subtraction_c4(gpu, golden, dt):
     got = out.cpu().numpy()
     del out
     ref, ref_bins = co.renormalize(x, badchans_mask=bad, cut_outliers=True, zero_dm=True, return_badbins=True)
-    np.testing.assert_array_equal(bins, ref_bins)
+    np.testing.assert_array_equal(bins.cpu().numpy(), ref_bins)
     assert np.array_equal(got, ref), np.argwhere(got != ref)[:5]
     # the subtraction removes the good channels' per-time-bin mean (up to rounding)
     good = ~bad
@@ -150,7 +150,7 @@ def test_cut_outliers_device_certified(gpu):
         bad[0] = True
         out, bins = C.renormalize_device(_hip.to_device(x), badchans_mask=bad, cut_outliers=True)
         ref, ref_bins = co.renormalize(x, badchans_mask=bad, cut_outliers=True, return_badbins=True)
-        np.testing.assert_array_equal(bins, ref_bins)
+        np.testing.assert_array_equal(bins.cpu().numpy(), ref_bins)
         np.testing.assert_array_equal(out.cpu().numpy(), ref)
     x = (rng.random((8, 500)) * 5 + 10)
     x[3, 100] = np.nan
