@@ -309,7 +309,7 @@ def main():
             roof.update({"hbm_counter_GBps": round(traffic / (kernel_ms / 1e3) / 1e9, 1),
                          "hbm_counter_frac": round(traffic / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                          "traffic_source": pmc.get("source"), "traffic_kernel_ms_at_collection":
-                             pmc.get("kernel_ms")})
+                             pmc.get("kernel_ms_at_collection")})
         if info["group"] > 1:
             # executed work of the exact subband decomposition: G x fewer
             # adds than the algorithm's; the LDS array (256 B/clk/CU) is its binding unit

@@ -30,6 +30,16 @@ fi
 if [ -n "$CLEANSWEEP" ]; then
   timeout -k 10 400 python -u scripts/sweep_clean.py > gpurun_out/${TAG}_sweep_clean.jsonl 2>&1 || exit $?
 fi
+if [ -n "$STRONG" ]; then
+  # per-rank kernel time of a strong-scaled run (total grid / N trials per GPU), N = 1, 2, 4, 8
+  for cfg in C2 C3; do
+    full=$([ $cfg = C2 ] && echo 1000 || echo 5000)
+    for nr in 1 2 4 8; do
+      echo "config=$cfg ranks=$nr trials=$((full / nr))" >> gpurun_out/${TAG}_strong.log
+      PU_TRIALS=$((full / nr)) PU_SWEEP=$([ $cfg = C2 ] && echo 4:160:0 || echo 8:160:0) PU_ROUNDS=1 timeout -k 10 300 python3 scripts/sweep.py $cfg >> gpurun_out/${TAG}_strong.log 2>&1 || exit $?
+    done
+  done
+fi
 if [ -n "$PROFILE" ]; then
   export TMPDIR=/tmp
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/${TAG}_prof.log 2>&1 || exit $?
