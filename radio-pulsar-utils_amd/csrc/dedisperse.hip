@@ -567,7 +567,7 @@ struct SubArgs {
     int32_t zero_len;       // floats of the zero row at LDS offset 0 (DMA mode, partial groups)
     int32_t lds_bytes;      // dynamic LDS size: a stage's raw rows end here
     int32_t skip;           // tuning ablation (PU_SUB_SKIP; results invalid): 1 build, 2 sum, 4 DMA
-    int32_t pad2;
+    int32_t dma_waves;      // waves that issue the LDS-DMA rows (the last ones of the workgroup)
     void *stamps;           // diagnostic build (PU_STAMPS): 8 x u64 phase-cycle totals
 };
 
@@ -776,13 +776,20 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
     // bases, lane k holding row wave + W k (one vector load per stage, issued a phase
     // ahead: a scalar load per row put its latency in series with every row's DMA issue,
     // ~10 % of the kernel's wave cycles at C2)
+    // Only the last NDW waves issue the DMA (rows dw + NDW k, dw = wave - (W - NDW)): the
+    // other waves go straight from the barrier to the sum instead of queueing their DMA
+    // instructions behind everyone's on the CU's one texture-address path.
     const int32_t *base_t = base_tab + (size_t)dt * o.nchan;
+    const int NDW = a.dma_waves;
+    const int dw = wave - (W - NDW);  // < 0: this wave issues no DMA
     auto bases_of = [&](const i32x4 st) -> int {
-        const int c = st.x * G + wave + W * lane;
-        return c < min(st.y * G, o.nchan) ? base_t[c] : 0;
+        const int c = st.x * G + dw + NDW * lane;
+        return dw >= 0 && c < min(st.y * G, o.nchan) ? base_t[c] : 0;
     };
-    // this wave's rows of stage st: wave + W k for k < rows_of(st)
-    auto rows_of = [&](const i32x4 st) { return (min(st.y * G, o.nchan) - st.x * G - wave + W - 1) / W; };
+    // this wave's rows of stage st: dw + NDW k for k < rows_of(st)
+    auto rows_of = [&](const i32x4 st) {
+        return dw < 0 ? 0 : (min(st.y * G, o.nchan) - st.x * G - dw + NDW - 1) / NDW;
+    };
     // rows k in [kb, ke) of this wave
     auto issue_raw = [&](const i32x4 st, int vb, int kb, int ke) {
         const int c0 = st.x * G;
@@ -792,7 +799,7 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
         unsigned char *raw = smem + a.lds_bytes - ((nc * a.raw_stride * EB + 255) & ~255);
         const int cover_bytes = (tile.z * EB + 255) & ~255;
         for (int k = kb; k < ke; ++k) {
-            const int ci = wave + W * k;
+            const int ci = dw + NDW * k;
             const int c = c0 + ci;
             int start = (k < 64 ? __builtin_amdgcn_readlane(vb, k) : ld_uniform(base_t + c)) + t0;
             if (start >= n) start -= n;
@@ -1169,6 +1176,8 @@ int launch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
     sa.lds_bytes = (int32_t)p->lds_bytes;
     if (const char *env = getenv("PU_SUB_SKIP")) sa.skip = atoi(env);
     sa.stamps = p->d_stamps;
+    sa.dma_waves = std::min<int>(8, C::W);  // C2 17.6 vs 18.95 ms with all 16 waves, C3 141 vs 150 (625 trials)
+    if (const char *env = getenv("PU_DMA_WAVES")) sa.dma_waves = std::clamp(atoi(env), 1, (int)C::W);
     const dim3 grid((unsigned)((int64_t)p->ndt * a.ntt_run)), block(C::THREADS);
     auto go = [&](auto kern) {
         int rc = ensure_lds(kern, p->lds_bytes);
