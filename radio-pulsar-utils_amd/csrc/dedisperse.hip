@@ -954,7 +954,13 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
             // the next stage's rows land while this stage is summed.  (Spreading these DMAs
             // over the sum's groups instead was measured slower, 20.6 vs 18.5 ms at C2: the
             // issue inside the sum breaks its read pipelining.)
-            if (k + 1 < ns && !(a.skip & 4)) issue_raw(st1, vb1, 0, rows_of(st1));
+            // The row-base load is waited for HERE, on every path, while no DMA is in
+            // flight: left to the compiler, the wait for it lands at the head of the sum
+            // loop as vmcnt(0) (its register is reused there), which also waits for all
+            // the DMAs just issued - every DMA wave then summed only after its rows landed.
+            int vb = vb1;
+            asm volatile("" : "+v"(vb));
+            if (k + 1 < ns && !(a.skip & 4)) issue_raw(st1, vb, 0, rows_of(st1));
         }
         PU_PHASE(4);
         if (active && !(a.skip & 2)) {
