@@ -232,16 +232,25 @@ __device__ __forceinline__ double wave_sum_to63_acc(Ta v)
     }
 }
 
+// max for values that are never NaN on the left (running maxima start at -inf and a NaN
+// candidate is skipped, as fmax skips it): a compare and a select, where fmax in IEEE
+// mode costs two canonicalising maxes on top
+template <typename T>
+__device__ __forceinline__ T max_nn(T a, T b)
+{
+    return b > a ? b : a;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_max_to63(T v)
 {
     const T lo = -INFINITY;
-    v = fmax(v, dpp<0xB1>(lo, v));
-    v = fmax(v, dpp<0x4E>(lo, v));
-    v = fmax(v, dpp<0x124>(lo, v));
-    v = fmax(v, dpp<0x128>(lo, v));
-    v = fmax(v, dpp<0x142, 0xA>(lo, v));
-    v = fmax(v, dpp<0x143, 0xC>(lo, v));
+    v = max_nn(v, dpp<0xB1>(lo, v));
+    v = max_nn(v, dpp<0x4E>(lo, v));
+    v = max_nn(v, dpp<0x124>(lo, v));
+    v = max_nn(v, dpp<0x128>(lo, v));
+    v = max_nn(v, dpp<0x142, 0xA>(lo, v));
+    v = max_nn(v, dpp<0x143, 0xC>(lo, v));
     return v;
 }
 
@@ -297,7 +306,7 @@ __device__ __forceinline__ void write_outputs(const Ta (&acc)[D][K], const Dedis
                 const int width = 1 << w;
                 if (lane_ok && t + width <= n) {
                     const Ta y = r - Ta(width) * kt;
-                    mx[w] = fmax(mx[w], r);
+                    mx[w] = max_nn(mx[w], r);
                     s1[w] += y;
                     s2[w] += y * y;
                 }
