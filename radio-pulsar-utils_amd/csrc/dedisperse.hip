@@ -136,8 +136,10 @@ __device__ __forceinline__ void pin_accumulators(Ta (&acc)[K])
     if constexpr (K == 8)
         asm volatile("" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]),
                      "+v"(acc[6]), "+v"(acc[7]));
-    else
+    else if constexpr (K == 4)
         asm volatile("" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]));
+    else
+        asm volatile("" : "+v"(acc[0]), "+v"(acc[1]));
 }
 
 template <typename Tl>
@@ -636,9 +638,18 @@ __device__ __forceinline__ void issue_window(double (&w)[J], uint32_t addr)
 }
 
 // One group's contribution to the wave's D trials: rec[d] = LDS byte offset (slot area
-// relative) of trial d's window; reads run 3 trials ahead of the adds.
+// relative) of trial d's window; reads run 3 trials ahead of the adds.  Accumulators are
+// float pairs (samples 2l + 128 j + {0, 1}): one window read is one pair, added by one
+// v_pk_add_f32 - two IEEE adds, the same bits as two v_add_f32, at half the VALU issue
+// (the sum's 8 v_add_f32 per trial took as many CU cycles as its 4 ds_read_b64).
+// (Skipping the reads of windows that repeat the previous trial's - a third of them at
+// C2 - was tried: 32 compile-time read patterns chosen per (group, wave) spilled at the
+// switch's joins; an EXEC = 0 ds_read_b64 or a ds_nop costs about as much as a real
+// read, scripts/lds_probe.hip.)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 template <class C, typename RecT>
-__device__ __forceinline__ void group_trials(float (&acc)[C::D][C::K], const RecT rec, uint32_t base)
+__device__ __forceinline__ void group_trials(f32x2 (&acc)[C::D][C::J], const RecT rec, uint32_t base)
 {
     constexpr int D = C::D, J = C::J;
     double w[4][J];
@@ -659,10 +670,7 @@ __device__ __forceinline__ void group_trials(float (&acc)[C::D][C::K], const Rec
         else
             wait_window_n<J, 0>(wd);
 #pragma unroll
-        for (int k = 0; k < C::K; ++k) {
-            const uint64_t bits = __builtin_bit_cast(uint64_t, wd[k >> 1]);
-            acc[d][k] += __builtin_bit_cast(float, (uint32_t)((k & 1) ? (bits >> 32) : bits));
-        }
+        for (int m = 0; m < J; ++m) acc[d][m] += __builtin_bit_cast(f32x2, wd[m]);
         pin_accumulators(acc[d]);
     }
 }
@@ -768,11 +776,11 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
     const float *raw_lds = reinterpret_cast<const float *>(smem);
     const unsigned char *raw_lds8 = smem;
 
-    float acc[D][K];
+    f32x2 acc2[D][C::J];
 #pragma unroll
     for (int d = 0; d < D; ++d)
 #pragma unroll
-        for (int k = 0; k < K; ++k) acc[d][k] = 0.0f;
+        for (int m = 0; m < C::J; ++m) acc2[d][m] = f32x2{0.0f, 0.0f};
 
     const rec_t *recs = reinterpret_cast<const rec_t *>(rec_tab) + (size_t)dt * a.ngroups * W + wave;
     if constexpr (kDma) {
@@ -976,8 +984,11 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
             const uint32_t sb = smem_addr + 8u * lane;  // window records: absolute LDS offsets
             rec_t rec = rec0;
             for (int g = st.x; g < st.y; ++g) {
-                const rec_t next = g + 1 < st.y ? ld_uniform(recs + (size_t)(g + 1) * W) : rec;
-                group_trials<C>(acc, rec, sb);
+                rec_t next = g + 1 < st.y ? ld_uniform(recs + (size_t)(g + 1) * W) : rec;
+                group_trials<C>(acc2, rec, sb);
+                // the next record is consumed only here, after the group's last lgkmcnt(0):
+                // hoisted into the loop, its scalar-load wait drained the LDS read pipeline
+                asm volatile("" : "+s"(next));
                 rec = next;
             }
         }
@@ -985,6 +996,14 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
         st = st1;
         st1 = st2;
     }
+    float acc[D][K];
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+        for (int m = 0; m < C::J; ++m) {
+            acc[d][2 * m] = acc2[d][m].x;
+            acc[d][2 * m + 1] = acc2[d][m].y;
+        }
 #ifdef PU_STAMPS
     if (active && !(a.skip & 8)) write_outputs<float, float, K, D, PLANE, STATS>(acc, o, first, slot0, cnt, t0, tt, lane);
     PU_PHASE(6);
