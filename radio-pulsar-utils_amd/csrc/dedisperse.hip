@@ -256,6 +256,107 @@ __device__ __forceinline__ T wave_max_to63(T v)
     return v;
 }
 
+// max(v, v of the DPP source lane) in one v_max_f32_dpp (rows outside ROW_MASK keep v).
+// IEEE-mode v_max_f32 returns the non-NaN operand, as fmax does; hipcc's fmax would
+// add canonicalising maxes and could not fold the DPP move.
+#define PU_MAX_DPP(NAME, CTRL)                                                                  \
+    __device__ __forceinline__ float NAME(float v)                                              \
+    {                                                                                           \
+        float r = v;                                                                            \
+        asm volatile("v_max_f32_dpp %0, %1, %0 " CTRL " bank_mask:0xf" : "+v"(r) : "v"(v));     \
+        return r;                                                                               \
+    }
+PU_MAX_DPP(max_qp1032, "quad_perm:[1,0,3,2] row_mask:0xf")
+PU_MAX_DPP(max_qp2301, "quad_perm:[2,3,0,1] row_mask:0xf")
+PU_MAX_DPP(max_ror4, "row_ror:4 row_mask:0xf")
+PU_MAX_DPP(max_ror8, "row_ror:8 row_mask:0xf")
+PU_MAX_DPP(max_bc15, "row_bcast:15 row_mask:0xa")
+PU_MAX_DPP(max_bc31, "row_bcast:31 row_mask:0xc")
+#undef PU_MAX_DPP
+
+__device__ __forceinline__ float wave_max_to63_dpp(float v)
+{
+    v = max_qp1032(v);
+    v = max_qp2301(v);
+    v = max_ror4(v);
+    v = max_ror8(v);
+    v = max_bc15(v);
+    return max_bc31(v);
+}
+
+__device__ __forceinline__ float vmax(float a, float b)
+{
+    float r;
+    asm volatile("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Search-mode outputs of a wave of the subband kernel for a FULL time tile (every width's
+// windows inside the series): the statistics of write_outputs (same partial record) from
+// the packed accumulator pairs, without per-sample bounds tests.  The width-1 and -2
+// accounting runs on pairs (v_pk_*); the width-4 and -8 sums come from DPP row shifts and
+// count only on lanes where they are aligned windows (a select, not a branch); maxima by
+// v_max_f32 and the wave reduction of maxima by v_max_f32_dpp.
+template <int D, int J>
+__device__ __forceinline__ void stats_full_pairs(const f32x2 (&acc)[D][J], const DedispArgs &a, int first, int slot0,
+                                                 int cnt, int tt, int lane)
+{
+    const bool even = (lane & 1) == 0, quad = (lane & 3) == 0;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        if (slot0 + d >= cnt) continue;
+        const float kt = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, acc[d][0].x), 0));
+        const f32x2 k1 = {kt, kt}, k2 = {2.0f * kt, 2.0f * kt}, k4 = {4.0f * kt, 4.0f * kt},
+                    k8 = {8.0f * kt, 8.0f * kt};
+        f32x2 s1 = {0.0f, 0.0f}, q1 = s1, q2 = s1, q4 = s1, q8 = s1;
+        float m1 = -INFINITY, m2 = -INFINITY, m4 = -INFINITY, m8 = -INFINITY;
+        float r1[J];
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const f32x2 x = acc[d][j];
+            const f32x2 y = x - k1;
+            s1 += y;
+            q1 += y * y;
+            m1 = vmax(m1, vmax(x.x, x.y));
+            r1[j] = x.x + x.y;  // width 2
+        }
+#pragma unroll
+        for (int j = 0; j < J; j += 2) {
+            const f32x2 r2 = {r1[j], r1[j + 1]};
+            const f32x2 y2 = r2 - k2;
+            q2 += y2 * y2;
+            m2 = vmax(m2, vmax(r2.x, r2.y));
+            f32x2 r4 = r2 + f32x2{row_down<1>(r2.x), row_down<1>(r2.y)};  // width 4 (even lanes)
+            const f32x2 y4 = r4 - k4;
+            const f32x2 z4 = y4 * y4;
+            q4 += f32x2{even ? z4.x : 0.0f, even ? z4.y : 0.0f};
+            m4 = vmax(m4, even ? vmax(r4.x, r4.y) : -INFINITY);
+            const f32x2 r8 = r4 + f32x2{row_down<2>(r4.x), row_down<2>(r4.y)};  // width 8 (lanes 4k)
+            const f32x2 y8 = r8 - k8;
+            const f32x2 z8 = y8 * y8;
+            q8 += f32x2{quad ? z8.x : 0.0f, quad ? z8.y : 0.0f};
+            m8 = vmax(m8, quad ? vmax(r8.x, r8.y) : -INFINITY);
+        }
+        double *p = a.partials + ((size_t)(first + slot0 + d) * a.ntt + tt) * kPartStride;
+        const double x1 = wave_sum_to63_acc<float>(s1.x + s1.y);
+        const float mw[4] = {wave_max_to63_dpp(m1), wave_max_to63_dpp(m2), wave_max_to63_dpp(m4),
+                             wave_max_to63_dpp(m8)};
+        const double xq[4] = {wave_sum_to63_acc<float>(q1.x + q1.y), wave_sum_to63_acc<float>(q2.x + q2.y),
+                              wave_sum_to63_acc<float>(q4.x + q4.y), wave_sum_to63_acc<float>(q8.x + q8.y)};
+        if (lane == 63) {
+            p[0] = static_cast<double>(kt);
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                p[1 + 3 * w] = static_cast<double>(mw[w]);
+                p[2 + 3 * w] = x1;
+                p[3 + 3 * w] = xq[w];
+            }
+        }
+    }
+}
+
 // Outputs of one wave: the dedispersed plane rows of its D trials, or their per-tile
 // partial statistics (1/2/4/8-sample rebinned sums: max, shifted sum, shifted sum of
 // squares; lane-local in the accumulation type, then float64 wave reductions).
@@ -646,7 +747,6 @@ __device__ __forceinline__ void issue_window(double (&w)[J], uint32_t addr)
 // C2 - was tried: 32 compile-time read patterns chosen per (group, wave) spilled at the
 // switch's joins; an EXEC = 0 ds_read_b64 or a ds_nop costs about as much as a real
 // read, scripts/lds_probe.hip.)
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <class C, typename RecT>
 __device__ __forceinline__ void group_trials(f32x2 (&acc)[C::D][C::J], const RecT rec, uint32_t base)
@@ -995,6 +1095,14 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
         PU_PHASE(5);
         st = st1;
         st1 = st2;
+    }
+    if constexpr (STATS && !PLANE) {
+        if (active && !(a.skip & 8) && t0 + TT <= n) {
+            stats_full_pairs<D, C::J>(acc2, o, first, slot0, cnt, tt, lane);
+#ifndef PU_STAMPS
+            return;
+#endif
+        }
     }
     float acc[D][K];
 #pragma unroll
