@@ -1080,6 +1080,11 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
             if (k + 1 < ns && !(a.skip & 4)) issue_raw(st1, vb, 0, rows_of(st1));
         }
         PU_PHASE(4);
+        // The DMA waves start summing last (their LDS-DMA issue holds them ~10 % of the
+        // stage), so they sum at raised priority: the other waves fill the LDS queue
+        // around them instead of reaching the barrier first and leaving it half idle
+        // (C2 17.3 -> 16.9 ms; raising it for the DMA issue too: 17.6).
+        if (dw >= 0) __builtin_amdgcn_s_setprio(1);
         if (active && !(a.skip & 2)) {
             const uint32_t sb = smem_addr + 8u * lane;  // window records: absolute LDS offsets
             rec_t rec = rec0;
@@ -1092,6 +1097,7 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
                 rec = next;
             }
         }
+        if (dw >= 0) __builtin_amdgcn_s_setprio(0);
         PU_PHASE(5);
         st = st1;
         st1 = st2;
@@ -1320,6 +1326,7 @@ int launch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
     sa.stamps = p->d_stamps;
     sa.dma_waves = std::min<int>(8, C::W);  // C2 17.6 vs 18.95 ms with all 16 waves, C3 141 vs 150 (625 trials)
     if (const char *env = getenv("PU_DMA_WAVES")) sa.dma_waves = std::clamp(atoi(env), 1, (int)C::W);
+
     const dim3 grid((unsigned)((int64_t)p->ndt * a.ntt_run)), block(C::THREADS);
     auto go = [&](auto kern) {
         int rc = ensure_lds(kern, p->lds_bytes);
