@@ -1107,6 +1107,8 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
             stats_full_pairs<D, C::J>(acc2, o, first, slot0, cnt, tt, lane);
 #ifndef PU_STAMPS
             return;
+#else
+            a.skip |= 8;  // stamps build: the epilogue is done, only the stamps remain
 #endif
         }
     }
