@@ -342,6 +342,56 @@ gauss_lds_kernel(const double *__restrict__ x, int64_t n, const double *__restri
     out[i] = acc;
 }
 
+// Pair form (r <= kGaussMaxR): each thread computes TWO adjacent outputs i, i+1 and steps
+// two taps at a time through 16-B LDS reads (x pairs and weight pairs): per 2 taps one
+// new left pair, one new right pair and one weight pair serve 4 output-taps, 3 LDS reads
+// where the one-output form needs 6.  Same per-output order as scipy (and as
+// gauss_lds_kernel): acc = x[i] w[r], then acc += (x[i+j] + x[i-j]) w[r+j], j = -r..-1.
+constexpr int kGaussPad = 2;
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+__global__ void __launch_bounds__(256)
+gauss_pair_kernel(const double *__restrict__ x, int64_t n, const double *__restrict__ w, int r,
+                  double *__restrict__ out)
+{
+    extern __shared__ __attribute__((aligned(16))) double gsm2[];
+    const int wn = (r + 2) & ~1;  // weights padded to an even count: the window stays 16-B aligned
+    double *ws = gsm2;
+    double *xs = gsm2 + wn;       // x[i0 - r - pad, i0 + 512 + r + pad), reflected at staging
+    const int64_t i0 = (int64_t)blockIdx.x * 512;
+    const int span = 512 + 2 * r + 2 * kGaussPad;
+    for (int k = threadIdx.x; k < wn; k += 256) ws[k] = k <= r ? w[k] : 0.0;
+    for (int k = threadIdx.x; k < span; k += 256) {
+        const int64_t g = i0 - r - kGaussPad + k;
+        xs[k] = x[(g >= 0 && g < n) ? g : reflect_index(g, n)];
+    }
+    __syncthreads();
+    const int t2 = 2 * (int)threadIdx.x;
+    const int64_t i = i0 + t2;
+    const double *xc = xs + t2 + r + kGaussPad;  // xc[q] = x[i + q]; xc + j is 16-B aligned for j = -r + 2m
+    double a0 = xc[0] * ws[r], a1 = xc[1] * ws[r];
+    int j = -r;
+    f64x2 L01 = *reinterpret_cast<const f64x2 *>(xc + j);  // x[i+j], x[i+j+1]
+    f64x2 R23 = *reinterpret_cast<const f64x2 *>(xc - j);  // x[i-j], x[i-j+1]
+    for (; j + 1 < 0; j += 2) {
+        const f64x2 L23 = *reinterpret_cast<const f64x2 *>(xc + j + 2);      // x[i+j+2], x[i+j+3]
+        const f64x2 R01 = *reinterpret_cast<const f64x2 *>(xc - j - 2);      // x[i-j-2], x[i-j-1]
+        const f64x2 wp = *reinterpret_cast<const f64x2 *>(ws + r + j);       // w[r+j], w[r+j+1]
+        a0 += (L01.x + R23.x) * wp.x;  // tap j
+        a1 += (L01.y + R23.y) * wp.x;
+        a0 += (L01.y + R01.y) * wp.y;  // tap j + 1
+        a1 += (L23.x + R23.x) * wp.y;
+        L01 = L23;
+        R23 = R01;
+    }
+    if (j < 0) {  // odd r: the last tap, j = -1
+        a0 += (L01.x + R23.x) * ws[r - 1];
+        a1 += (L01.y + R23.y) * ws[r - 1];
+    }
+    if (i < n) out[i] = a0;
+    if (i + 1 < n) out[i + 1] = a1;
+}
+
 __global__ void ratio_kernel(double num, const double *__restrict__ x, int64_t n, double *__restrict__ out)
 {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -985,10 +1035,20 @@ int pu_gaussian_filter1d(const double *x, int64_t n, const double *w, int64_t r,
 {
     PU_REQUIRE(x && w && out && n > 0 && r >= 0, "pu_gaussian_filter1d: bad arguments");
     if (r <= kGaussMaxR) {
-        const size_t lds = (size_t)(r + 1 + 256 + 2 * r) * sizeof(double);
-        hipLaunchKernelGGL(gauss_lds_kernel, dim3(blocks_for(n, 256)), dim3(256), lds, pu::as_stream(stream), x, n, w,
-                           (int)r, out);
-        return pu::launch_check("gauss_lds_kernel");
+        static const bool single = [] {
+            const char *e = getenv("PU_GAUSS_SINGLE");  // the one-output form, for A/B
+            return e && atoi(e) != 0;
+        }();
+        if (single) {
+            const size_t lds = (size_t)(r + 1 + 256 + 2 * r) * sizeof(double);
+            hipLaunchKernelGGL(gauss_lds_kernel, dim3(blocks_for(n, 256)), dim3(256), lds, pu::as_stream(stream), x,
+                               n, w, (int)r, out);
+            return pu::launch_check("gauss_lds_kernel");
+        }
+        const size_t lds = (size_t)(((r + 2) & ~int64_t(1)) + 512 + 2 * r + 2 * kGaussPad) * sizeof(double);
+        hipLaunchKernelGGL(gauss_pair_kernel, dim3(blocks_for(n, 512)), dim3(256), lds, pu::as_stream(stream), x, n,
+                           w, (int)r, out);
+        return pu::launch_check("gauss_pair_kernel");
     }
     hipLaunchKernelGGL(gauss_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, pu::as_stream(stream), x, n, w, r, out);
     return pu::launch_check("gauss_kernel");

@@ -191,3 +191,22 @@ def test_median_device_matches_numpy(gpu, n):
         want = np.median(a)
         assert np.array_equal(np.array([got]), np.array([want]), equal_nan=True), (n, got, want)
         assert np.signbit(got) == np.signbit(want)
+
+
+@pytest.mark.parametrize("n,sigma", [(12345, 101), (262144, 101), (1000, 3), (777, 2.6), (3001, 2.7), (50, 7),
+                                     (10, 5), (1, 1), (513, 0.2)])
+def test_gaussian_filter1d_vs_scipy(gpu, n, sigma):
+    """pu_gaussian_filter1d (the pair kernel; odd radii 11 and 1 exercise its last-tap
+    path, n < radius the repeated reflection) equals scipy's gaussian_filter1d bit for bit."""
+    import torch
+    from scipy.ndimage import gaussian_filter1d
+    from pulsarutils import _hip
+    rng = np.random.default_rng(n)
+    x = rng.normal(size=n) * 10 + 100
+    dw, radius = C._gaussian_weights_device(sigma, torch.device("cuda", 0))
+    xd = torch.from_numpy(x).cuda()
+    out = torch.empty_like(xd)
+    lib = _hip.lib()
+    _hip.check(lib.pu_gaussian_filter1d(_hip.ptr(xd), n, _hip.ptr(dw), radius, _hip.ptr(out), _hip.stream_ptr()),
+               "pu_gaussian_filter1d")
+    np.testing.assert_array_equal(out.cpu().numpy(), gaussian_filter1d(x, sigma, mode="reflect"))
