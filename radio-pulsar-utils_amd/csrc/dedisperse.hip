@@ -192,6 +192,22 @@ __device__ __forceinline__ T dpp(T old, T v)
     }
 }
 
+// The DPP-moved value with no "old" operand (v_mov_b32_dpp into a fresh register): lanes
+// of rows outside ROW_MASK get an undefined value.  For reductions whose result is read
+// from lane 63 only, this drops the zeroing move that update_dpp(0, v) costs per dword.
+template <int CTRL, int ROW_MASK = 0xf, typename T>
+__device__ __forceinline__ T dpp_undef(T v)
+{
+    if constexpr (sizeof(T) == 4) {
+        return __builtin_bit_cast(T, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xf, true));
+    } else {
+        const uint64_t x = __builtin_bit_cast(uint64_t, v);
+        const uint64_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)x, CTRL, ROW_MASK, 0xf, true);
+        const uint64_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(x >> 32), CTRL, ROW_MASK, 0xf, true);
+        return __builtin_bit_cast(T, lo | (hi << 32));
+    }
+}
+
 // Value of lane l + S within the lane's row of 16 (row_shl:S); lanes past the row end
 // get 0.  Used only where l + S stays in the row.
 template <int S, typename T>
@@ -202,15 +218,17 @@ __device__ __forceinline__ T row_down(T v)
 
 // Wave reductions to lane 63: within rows (quad xor 1, 2, row_ror 4, 8), then
 // row_bcast15 into rows 1 and 3, row_bcast31 into rows 2 and 3.
+// (Only lane 63's result is defined: the row_bcast steps leave rows outside their mask
+// with undefined partial sums.)
 template <typename T>
 __device__ __forceinline__ T wave_sum_to63(T v)
 {
-    v += dpp<0xB1>(T(0), v);
-    v += dpp<0x4E>(T(0), v);
-    v += dpp<0x124>(T(0), v);
-    v += dpp<0x128>(T(0), v);
-    v += dpp<0x142, 0xA>(T(0), v);
-    v += dpp<0x143, 0xC>(T(0), v);
+    v += dpp_undef<0xB1>(v);
+    v += dpp_undef<0x4E>(v);
+    v += dpp_undef<0x124>(v);
+    v += dpp_undef<0x128>(v);
+    v += dpp_undef<0x142, 0xA>(v);
+    v += dpp_undef<0x143, 0xC>(v);
     return v;
 }
 
@@ -223,13 +241,13 @@ __device__ __forceinline__ double wave_sum_to63_acc(Ta v)
     if constexpr (sizeof(Ta) == 8) {
         return wave_sum_to63(v);
     } else {
-        v += dpp<0xB1>(Ta(0), v);
-        v += dpp<0x4E>(Ta(0), v);
-        v += dpp<0x124>(Ta(0), v);
-        v += dpp<0x128>(Ta(0), v);
+        v += dpp_undef<0xB1>(v);
+        v += dpp_undef<0x4E>(v);
+        v += dpp_undef<0x124>(v);
+        v += dpp_undef<0x128>(v);
         double r = static_cast<double>(v);
-        r += dpp<0x142, 0xA>(0.0, r);
-        r += dpp<0x143, 0xC>(0.0, r);
+        r += dpp_undef<0x142, 0xA>(r);
+        r += dpp_undef<0x143, 0xC>(r);
         return r;
     }
 }
@@ -287,7 +305,7 @@ __device__ __forceinline__ float wave_max_to63_dpp(float v)
 __device__ __forceinline__ float vmax(float a, float b)
 {
     float r;
-    asm volatile("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));  // pure: may be computed unconditionally
     return r;
 }
 
@@ -295,10 +313,12 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // Search-mode outputs of a wave of the subband kernel for a FULL time tile (every width's
 // windows inside the series): the statistics of write_outputs (same partial record) from
-// the packed accumulator pairs, without per-sample bounds tests.  The width-1 and -2
-// accounting runs on pairs (v_pk_*); the width-4 and -8 sums come from DPP row shifts and
-// count only on lanes where they are aligned windows (a select, not a branch); maxima by
-// v_max_f32 and the wave reduction of maxima by v_max_f32_dpp.
+// the packed accumulator pairs, without per-sample bounds tests.  Width 1 runs on the
+// pairs (v_pk_*); widths 2/4/8 on scalars (the 4- and 8-sample sums are single fused
+// v_add_f32_dpp row shifts - packing them would cost a DPP move per half) and count only
+// on lanes where they are aligned windows, by selects computed unconditionally (a
+// conditional v_max in inline asm became an EXEC-mask branch); maxima by v_max_f32 and the
+// wave reduction of maxima by v_max_f32_dpp.
 template <int D, int J>
 __device__ __forceinline__ void stats_full_pairs(const f32x2 (&acc)[D][J], const DedispArgs &a, int first, int slot0,
                                                  int cnt, int tt, int lane)
@@ -308,11 +328,11 @@ __device__ __forceinline__ void stats_full_pairs(const f32x2 (&acc)[D][J], const
     for (int d = 0; d < D; ++d) {
         if (slot0 + d >= cnt) continue;
         const float kt = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, acc[d][0].x), 0));
-        const f32x2 k1 = {kt, kt}, k2 = {2.0f * kt, 2.0f * kt}, k4 = {4.0f * kt, 4.0f * kt},
-                    k8 = {8.0f * kt, 8.0f * kt};
-        f32x2 s1 = {0.0f, 0.0f}, q1 = s1, q2 = s1, q4 = s1, q8 = s1;
+        const f32x2 k1 = {kt, kt};
+        const float k2 = 2.0f * kt, k4 = 4.0f * kt, k8 = 8.0f * kt;
+        f32x2 s1 = {0.0f, 0.0f}, q1 = s1;
+        float q2 = 0.0f, q4 = 0.0f, q8 = 0.0f;
         float m1 = -INFINITY, m2 = -INFINITY, m4 = -INFINITY, m8 = -INFINITY;
-        float r1[J];
 #pragma unroll
         for (int j = 0; j < J; ++j) {
             const f32x2 x = acc[d][j];
@@ -320,31 +340,25 @@ __device__ __forceinline__ void stats_full_pairs(const f32x2 (&acc)[D][J], const
             s1 += y;
             q1 += y * y;
             m1 = vmax(m1, vmax(x.x, x.y));
-            r1[j] = x.x + x.y;  // width 2
-        }
-#pragma unroll
-        for (int j = 0; j < J; j += 2) {
-            const f32x2 r2 = {r1[j], r1[j + 1]};
-            const f32x2 y2 = r2 - k2;
+            const float r2 = x.x + x.y;                 // width 2 (every lane)
+            const float y2 = r2 - k2;
             q2 += y2 * y2;
-            m2 = vmax(m2, vmax(r2.x, r2.y));
-            f32x2 r4 = r2 + f32x2{row_down<1>(r2.x), row_down<1>(r2.y)};  // width 4 (even lanes)
-            const f32x2 y4 = r4 - k4;
-            const f32x2 z4 = y4 * y4;
-            q4 += f32x2{even ? z4.x : 0.0f, even ? z4.y : 0.0f};
-            m4 = vmax(m4, even ? vmax(r4.x, r4.y) : -INFINITY);
-            const f32x2 r8 = r4 + f32x2{row_down<2>(r4.x), row_down<2>(r4.y)};  // width 8 (lanes 4k)
-            const f32x2 y8 = r8 - k8;
-            const f32x2 z8 = y8 * y8;
-            q8 += f32x2{quad ? z8.x : 0.0f, quad ? z8.y : 0.0f};
-            m8 = vmax(m8, quad ? vmax(r8.x, r8.y) : -INFINITY);
+            m2 = vmax(m2, r2);
+            const float r4 = r2 + row_down<1>(r2);      // width 4 (even lanes)
+            const float y4 = even ? r4 - k4 : 0.0f;
+            q4 += y4 * y4;
+            m4 = vmax(m4, even ? r4 : -INFINITY);
+            const float r8 = r4 + row_down<2>(r4);      // width 8 (lanes 4k)
+            const float y8 = quad ? r8 - k8 : 0.0f;
+            q8 += y8 * y8;
+            m8 = vmax(m8, quad ? r8 : -INFINITY);
         }
         double *p = a.partials + ((size_t)(first + slot0 + d) * a.ntt + tt) * kPartStride;
         const double x1 = wave_sum_to63_acc<float>(s1.x + s1.y);
         const float mw[4] = {wave_max_to63_dpp(m1), wave_max_to63_dpp(m2), wave_max_to63_dpp(m4),
                              wave_max_to63_dpp(m8)};
-        const double xq[4] = {wave_sum_to63_acc<float>(q1.x + q1.y), wave_sum_to63_acc<float>(q2.x + q2.y),
-                              wave_sum_to63_acc<float>(q4.x + q4.y), wave_sum_to63_acc<float>(q8.x + q8.y)};
+        const double xq[4] = {wave_sum_to63_acc<float>(q1.x + q1.y), wave_sum_to63_acc<float>(q2),
+                              wave_sum_to63_acc<float>(q4), wave_sum_to63_acc<float>(q8)};
         if (lane == 63) {
             p[0] = static_cast<double>(kt);
 #pragma unroll
