@@ -694,6 +694,7 @@ struct SubArgs {
     int32_t lds_bytes;      // dynamic LDS size: a stage's raw rows end here
     int32_t skip;           // tuning ablation (PU_SUB_SKIP; results invalid): 1 build, 2 sum, 4 DMA
     int32_t dma_waves;      // waves that issue the LDS-DMA rows (the last ones of the workgroup)
+    int32_t nitems;         // work items (DM tiles x time tiles of this launch)
     void *stamps;           // diagnostic build (PU_STAMPS): 8 x u64 phase-cycle totals
 };
 
@@ -852,11 +853,13 @@ __device__ __forceinline__ void dma_row_u8(unsigned char *dst, const unsigned ch
 
 // DMA8: 8-bit rows staged by LDS-DMA as bytes (plans with n % 4 == 0); otherwise 8-bit
 // and float64 builds read global memory.
+// One (DM tile, time tile) work item of the subband kernel: logical index wg; first =
+// this workgroup's first item (it writes the zero row, which no item overwrites).
 template <class C, typename Tin, int G, bool PLANE, bool STATS, bool DMA8>
-__global__ void __launch_bounds__(C::THREADS, 4)
-dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__restrict__ tile_stages,
-                  const i32x4 *__restrict__ stages, const int32_t *__restrict__ slots,
-                  const int32_t *__restrict__ base_tab, const uint32_t *__restrict__ rec_tab)
+__device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ tiles,
+                                         const i32x2 *__restrict__ tile_stages, const i32x4 *__restrict__ stages,
+                                         const int32_t *__restrict__ slots, const int32_t *__restrict__ base_tab,
+                                         const uint32_t *__restrict__ rec_tab, const int wg, const bool first_item)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr bool kDma = std::is_same<Tin, float>::value || (DMA8 && std::is_same<Tin, uint8_t>::value);
@@ -869,7 +872,6 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
     typedef uint32_t rec_t __attribute__((ext_vector_type(D)));
     const DedispArgs &o = a.o;
     const int ndt = o.ndt;
-    const int wg = pu::xcd_remap(blockIdx.x, gridDim.x);
     const int dt = wg % ndt;
     const int tt = o.tt0 + wg / ndt;
     const int t0 = tt * TT;
@@ -899,8 +901,10 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
     const rec_t *recs = reinterpret_cast<const rec_t *>(rec_tab) + (size_t)dt * a.ngroups * W + wave;
     if constexpr (kDma) {
         // zero row (partial groups' missing channels) between the raw rows and the slots
-        float *zero = reinterpret_cast<float *>(smem);
-        for (int i = tid; i < a.zero_len; i += C::THREADS) zero[i] = 0.0f;
+        if (first_item) {
+            float *zero = reinterpret_cast<float *>(smem);
+            for (int i = tid; i < a.zero_len; i += C::THREADS) zero[i] = 0.0f;
+        }
     }
 
     // ---- DMA mode: the channel rows of stage st into the raw area.  vb = this wave's row
@@ -1149,6 +1153,26 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
 #endif
 }
 
+// Persistent over the work items: workgroup b takes items b, b + grid, ... (grid a
+// multiple of 8, so an item stays on the XCD its index maps to, and xcd_remap gives the
+// 8 DM tiles of a time tile to one XCD as in the one-item-per-workgroup launch).  A
+// barrier between items: the next item's first LDS-DMA rows may overlap the slots the
+// last waves of this item are still summing.
+template <class C, typename Tin, int G, bool PLANE, bool STATS, bool DMA8>
+__global__ void __launch_bounds__(C::THREADS, 4)
+dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__restrict__ tile_stages,
+                  const i32x4 *__restrict__ stages, const int32_t *__restrict__ slots,
+                  const int32_t *__restrict__ base_tab, const uint32_t *__restrict__ rec_tab)
+{
+    const int skip0 = a.skip;
+    for (int item = blockIdx.x; item < a.nitems; item += gridDim.x) {
+        if (item != (int)blockIdx.x) __syncthreads();
+        a.skip = skip0;
+        sub_item<C, Tin, G, PLANE, STATS, DMA8>(a, tiles, tile_stages, stages, slots, base_tab, rec_tab,
+                                                pu::xcd_remap(item, a.nitems), item == (int)blockIdx.x);
+    }
+}
+
 // One workgroup per trial: combine the per-time-tile partials in a fixed order
 // (thread-strided then an LDS tree: deterministic), then the reference's S/N logic
 // (dedispersion.py:186-201): snr_w = max(reb_w)/std(reb_w), first strict best.
@@ -1343,7 +1367,26 @@ int launch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
     sa.dma_waves = std::min<int>(8, C::W);  // C2 17.6 vs 18.95 ms with all 16 waves, C3 141 vs 150 (625 trials)
     if (const char *env = getenv("PU_DMA_WAVES")) sa.dma_waves = std::clamp(atoi(env), 1, (int)C::W);
 
-    const dim3 grid((unsigned)((int64_t)p->ndt * a.ntt_run)), block(C::THREADS);
+    // one workgroup per item by default; PU_SUB_PERSIST=1: a persistent grid of one
+    // workgroup per CU (two for the 80 KiB pair shape), each taking every grid-th item -
+    // measured slower at C2 (16.68 vs 16.19 ms: the hardware's dynamic dispatch of the
+    // next workgroup to whichever CU frees first beats the static round-robin), equal at C5
+    const int64_t nitems = (int64_t)p->ndt * a.ntt_run;
+    sa.nitems = (int32_t)nitems;
+    int64_t nblk = nitems;
+    static const int persist = [] {
+        const char *e = getenv("PU_SUB_PERSIST");
+        return e ? atoi(e) : 0;
+    }();
+    if (persist) {
+        int dev = 0, ncu = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0) {
+            const int64_t per_cu = C::W == 8 ? 2 : 1;
+            nblk = std::min<int64_t>(nitems, ((int64_t)ncu * per_cu + 7) / 8 * 8);
+        }
+    }
+    const dim3 grid((unsigned)nblk), block(C::THREADS);
     auto go = [&](auto kern) {
         int rc = ensure_lds(kern, p->lds_bytes);
         if (rc) return rc;
