@@ -1153,24 +1153,18 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
 #endif
 }
 
-// Persistent over the work items: workgroup b takes items b, b + grid, ... (grid a
-// multiple of 8, so an item stays on the XCD its index maps to, and xcd_remap gives the
-// 8 DM tiles of a time tile to one XCD as in the one-item-per-workgroup launch).  A
-// barrier between items: the next item's first LDS-DMA rows may overlap the slots the
-// last waves of this item are still summing.
+// One workgroup per work item.  (A persistent grid - one workgroup per CU looping over
+// items b, b + grid, ... - measured slower at C2, 16.68 vs 16.19 ms: the hardware's
+// dynamic dispatch of the next workgroup to whichever CU frees first beats a static
+// round-robin; and its loop state cost the C3 instantiation scratch spills.)
 template <class C, typename Tin, int G, bool PLANE, bool STATS, bool DMA8>
 __global__ void __launch_bounds__(C::THREADS, 4)
 dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__restrict__ tile_stages,
                   const i32x4 *__restrict__ stages, const int32_t *__restrict__ slots,
                   const int32_t *__restrict__ base_tab, const uint32_t *__restrict__ rec_tab)
 {
-    const int skip0 = a.skip;
-    for (int item = blockIdx.x; item < a.nitems; item += gridDim.x) {
-        if (item != (int)blockIdx.x) __syncthreads();
-        a.skip = skip0;
-        sub_item<C, Tin, G, PLANE, STATS, DMA8>(a, tiles, tile_stages, stages, slots, base_tab, rec_tab,
-                                                pu::xcd_remap(item, a.nitems), item == (int)blockIdx.x);
-    }
+    sub_item<C, Tin, G, PLANE, STATS, DMA8>(a, tiles, tile_stages, stages, slots, base_tab, rec_tab,
+                                            pu::xcd_remap(blockIdx.x, gridDim.x), true);
 }
 
 // One workgroup per trial: combine the per-time-tile partials in a fixed order
@@ -1367,25 +1361,9 @@ int launch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
     sa.dma_waves = std::min<int>(8, C::W);  // C2 17.6 vs 18.95 ms with all 16 waves, C3 141 vs 150 (625 trials)
     if (const char *env = getenv("PU_DMA_WAVES")) sa.dma_waves = std::clamp(atoi(env), 1, (int)C::W);
 
-    // one workgroup per item by default; PU_SUB_PERSIST=1: a persistent grid of one
-    // workgroup per CU (two for the 80 KiB pair shape), each taking every grid-th item -
-    // measured slower at C2 (16.68 vs 16.19 ms: the hardware's dynamic dispatch of the
-    // next workgroup to whichever CU frees first beats the static round-robin), equal at C5
     const int64_t nitems = (int64_t)p->ndt * a.ntt_run;
     sa.nitems = (int32_t)nitems;
-    int64_t nblk = nitems;
-    static const int persist = [] {
-        const char *e = getenv("PU_SUB_PERSIST");
-        return e ? atoi(e) : 0;
-    }();
-    if (persist) {
-        int dev = 0, ncu = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0) {
-            const int64_t per_cu = C::W == 8 ? 2 : 1;
-            nblk = std::min<int64_t>(nitems, ((int64_t)ncu * per_cu + 7) / 8 * 8);
-        }
-    }
+    const int64_t nblk = nitems;
     const dim3 grid((unsigned)nblk), block(C::THREADS);
     auto go = [&](auto kern) {
         int rc = ensure_lds(kern, p->lds_bytes);
