@@ -695,6 +695,7 @@ struct SubArgs {
     int32_t skip;           // tuning ablation (PU_SUB_SKIP; results invalid): 1 build, 2 sum, 4 DMA
     int32_t dma_waves;      // waves that issue the LDS-DMA rows (the last ones of the workgroup)
     int32_t nitems;         // work items (DM tiles x time tiles of this launch)
+    int32_t base_bits;      // DMA row words: base = word & (2^base_bits - 1), cover = (word >> base_bits) x 256 B
     void *stamps;           // diagnostic build (PU_STAMPS): 8 x u64 phase-cycle totals
 };
 
@@ -932,11 +933,17 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
         // the stage's rows end at the top of LDS (the host packs stages so that they never
         // overlap the previous stage's slots, which are summed while these rows land)
         unsigned char *raw = smem + a.lds_bytes - ((nc * a.raw_stride * EB + 255) & ~255);
-        const int cover_bytes = (tile.z * EB + 255) & ~255;
+        const int cover_tile = (tile.z * EB + 255) & ~255;
+        const uint32_t base_mask = (1u << a.base_bits) - 1u;
         for (int k = kb; k < ke; ++k) {
             const int ci = dw + NDW * k;
             const int c = c0 + ci;
-            int start = (k < 64 ? __builtin_amdgcn_readlane(vb, k) : ld_uniform(base_t + c)) + t0;
+            // the row word: its base mod N and, in the top bits, this channel's own cover
+            // (TT + its shift spread over the tile, in 256-B units; 0 = the tile's)
+            const uint32_t word = (uint32_t)(k < 64 ? __builtin_amdgcn_readlane(vb, k) : ld_uniform(base_t + c));
+            const uint32_t cu = word >> a.base_bits;
+            const int cover_bytes = cu ? (int)(cu << 8) : cover_tile;
+            int start = (int)(word & base_mask) + t0;
             if (start >= n) start -= n;
             if constexpr (EB == 4)
                 dma_row_f32(raw + ci * a.raw_stride * 4,
@@ -1288,6 +1295,7 @@ struct pu_plan {
     // stages {group begin, group end, item begin, item end}, build items, window records
     int group = 1, ngroups = 0, nslots_total = 0, raw_stride = 0, shape = SUB_WIDE;
     int dma8 = 0;  // subband plan stages 8-bit rows by LDS-DMA (rows must be 4-byte aligned)
+    int base_bits = 31;  // subband DMA row words: base bits (24: per-channel cover above them)
     size_t slot_bytes = 0, zero_len = 0;
     int64_t exec_adds = 0, lds_traffic = 0;  // per launch (measurement: bench.py roofline)
     int64_t nstages = 0;
@@ -1363,6 +1371,7 @@ int launch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
 
     const int64_t nitems = (int64_t)p->ndt * a.ntt_run;
     sa.nitems = (int32_t)nitems;
+    sa.base_bits = p->base_bits;
     const int64_t nblk = nitems;
     const dim3 grid((unsigned)nblk), block(C::THREADS);
     auto go = [&](auto kern) {
@@ -1592,6 +1601,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     if (const char *env = getenv("PU_U8_DMA")) dma8 = dma8 && atoi(env) != 0;
     const bool dma = p->dtype == PU_F32 || dma8;
     const int64_t eb = dma8 ? 1 : 4;  // bytes per staged raw element
+    const bool pack_cover = n < (int64_t(1) << 24);  // row bases fit 24 bits: covers above them
     // a stage's raw rows (DMA mode) and its slots share the LDS budget; a stage holds
     // whole groups.  The zero row (DMA mode, partial last group) sits at the end.
     const bool partial = dma && nchan % G != 0;
@@ -1642,7 +1652,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     // ---- DM tiles: <= T consecutive trials whose channel rows (one group's worth)
     // fit the raw area and whose slots of any one group fit the slot area
     std::vector<int32_t> first, count;
-    std::vector<int64_t> spread_t, span_t, smin_t;  // smin_t: per tile x channel
+    std::vector<int64_t> spread_t, span_t, smin_t, smax_t;  // smin_t / smax_t: per tile x channel
     std::vector<std::vector<SubSlot>> tslots;       // per tile x group
     {
         std::vector<int64_t> mn((size_t)nchan), mx((size_t)nchan);
@@ -1695,6 +1705,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
             spread_t.push_back(spread);
             span_t.push_back(span);
             smin_t.insert(smin_t.end(), mn.begin(), mn.end());
+            smax_t.insert(smax_t.end(), mx.begin(), mx.end());
             for (int g = 0; g < ngroups; ++g) tslots.push_back(cur[g]);
             i = j;
         }
@@ -1748,13 +1759,24 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     for (int t = 0; t < ndt; ++t) {
         const int64_t cb = copy_of(span_t[t]);
         const int64_t *smin = smin_t.data() + (size_t)t * nchan;
+        const int64_t *smax = smax_t.data() + (size_t)t * nchan;
         const int64_t trials_run = (count[t] + D - 1) / D * D;  // active waves run all D trials
         adds_tile += trials_run * ngroups * TT;
         lds_tile += trials_run * ngroups * TT * 4;  // sum: one window read per trial and group
         const int64_t row_len = TT + spread_t[t] + 1 + (dma8 ? 3 : 0);  // staged elements per row
         tiles[t] = i32x4{first[t], count[t], (int32_t)row_len, (int32_t)cb};
         if (dma)
-            for (int64_t c = 0; c < nchan; ++c) base.push_back((int32_t)(dma8 ? base_of(smin[c]) & ~int64_t(3) : base_of(smin[c])));
+            for (int64_t c = 0; c < nchan; ++c) {
+                int64_t b = dma8 ? base_of(smin[c]) & ~int64_t(3) : base_of(smin[c]);
+                if (pack_cover) {
+                    // the channel's own DMA cover: its rows need TT + its spread + 1 (+3)
+                    // elements, not the tile's widest (C2: 2304 vs 2560 B for most rows)
+                    const int64_t len = TT + (smax[c] - smin[c]) + 1 + (dma8 ? 3 : 0);
+                    const int64_t cu = (len * eb + 255) / 256;
+                    if (cu < 128) b |= cu << 24;
+                }
+                base.push_back((int32_t)b);
+            }
         tile_stages[t] = i32x2{(int32_t)stages.size(), 0};
         prev_slots = 0;
         int g = 0;
@@ -1861,6 +1883,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     p->small_n = raw_stride + 2 > n ? 1 : 0;
     p->zero_len = zr ? (size_t)(((raw_stride + 64) * eb + 3) / 4) : 0;  // floats
     p->dma8 = dma8 ? 1 : 0;
+    p->base_bits = pack_cover ? 24 : 31;
     p->slot_bytes = (size_t)slot_used;
     p->lds_bytes = (size_t)lds_total;
     p->nslots_total = (int)(slotmeta.size() / ms);
