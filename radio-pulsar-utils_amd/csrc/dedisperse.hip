@@ -1048,14 +1048,9 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
     // slot over waves to balance the ~20 slots of a stage over 16 waves was measured
     // slower: 22.1 / 25.6 vs 20.2 ms for halves / thirds - fewer reads in flight per
     // pass, and the extra pass code spilled registers.)
-    // m0, m1: this wave's first and second slot records, loaded before the stage barrier
-    // (the waves that build a second slot end the phase; a record load between their
-    // two slots put its latency on that path)
-    auto build = [&](const i32x4 st, const meta_t m0, const meta_t m1) {
+    auto build = [&](const i32x4 st, const meta_t m0) {
         for (int s = st.z + wave; s < st.w; s += W) {
-            const meta_t m = s == st.z + wave       ? m0
-                             : s == st.z + wave + W ? m1
-                                                    : ld_uniform(reinterpret_cast<const meta_t *>(slots + (size_t)s * MS));
+            const meta_t m = s == st.z + wave ? m0 : ld_uniform(reinterpret_cast<const meta_t *>(slots + (size_t)s * MS));
             const int len = m[0], gs = m[3];
             const int lim = (len + 63) & ~63;
             for (int i0 = 0; i0 < len; i0 += 64 * U) build_pass(std::integral_constant<int, U>{}, m, gs, i0, lim);
@@ -1082,7 +1077,6 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
     for (int k = 0; k < ns; ++k) {
         const i32x4 st2 = stage_at(k + 2);
         const meta_t m0 = meta_of(st);
-        const meta_t m1 = ld_uniform(reinterpret_cast<const meta_t *>(slots + (size_t)min(st.z + wave + W, st.w - 1) * MS));
         const rec_t rec0 = ld_uniform(recs + (size_t)st.x * W);
         PU_PHASE(0);
         // This wave's LDS-DMA rows have landed before it arrives at the barrier.  Explicit:
@@ -1094,7 +1088,7 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
         __syncthreads();  // raw rows of stage k landed; every wave left the slot area
         PU_PHASE(1);
         const int vb1 = kDma && k + 1 < ns ? bases_of(st1) : 0;  // lands during the build
-        if (!(a.skip & 1)) build(st, m0, m1);
+        if (!(a.skip & 1)) build(st, m0);
         PU_PHASE(2);
         __syncthreads();  // slots built; every wave left the raw rows
         PU_PHASE(3);
