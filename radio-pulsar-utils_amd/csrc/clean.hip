@@ -294,6 +294,76 @@ colmean_kernel(const Tin *__restrict__ x, int64_t nrows, int64_t col0, int64_t n
     for (int j = 0; j < V; ++j) out[c + j] = acc[j] / static_cast<double>(ngood);
 }
 
+// 8-bit column sums by row segments.  Every partial sum of 8-bit values is an integer
+// (< 2^53), so float64 accumulation is exact in any order: the sequential chain of
+// colmean_kernel and a sum of per-segment integer sums give the same bits.  Segments of
+// kColSegRows rows fit u16 (256 x 255 = 65280), two columns per dword lane half
+// (bytes 0/2 and 1/3 masked with 0x00ff00ff: the halves never carry into each other), so a
+// row of 8 columns costs one 8-byte load and four adds.  The (up to 4) u16 segment sums of
+// column c are written into out[c]'s 8 bytes; colsum_u8_finish_kernel adds them and divides
+// in place.  4 x the lanes of the row-sequential kernel for the same bytes.
+constexpr int kColSegRows = 256;
+constexpr int kColSegMax = 4;
+
+__global__ void __launch_bounds__(256)
+colsum_u8_seg_kernel(const uint8_t *__restrict__ x, int64_t nrows, int64_t ncols, int64_t ld,
+                     const uint8_t *__restrict__ skip, uint16_t *__restrict__ part)
+{
+    __shared__ uint8_t sk[kColSegRows];
+    const int seg = blockIdx.y;
+    const int64_t r0 = (int64_t)seg * kColSegRows;
+    const int rn = (int)(nrows - r0 < kColSegRows ? nrows - r0 : kColSegRows);
+    if ((int)threadIdx.x < rn) sk[threadIdx.x] = skip ? skip[r0 + threadIdx.x] : 0;
+    __syncthreads();
+    const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+    if (c >= ncols) return;
+    const uint8_t *p = x + r0 * ld + c;
+    uint32_t a02 = 0, a13 = 0, a46 = 0, a57 = 0;  // u16 pairs: columns (0,2), (1,3), (4,6), (5,7)
+    constexpr int B = 16;                          // rows in flight per lane
+    for (int i0 = 0; i0 < rn; i0 += B) {
+        uint2 v[B];
+#pragma unroll
+        for (int k = 0; k < B; ++k)
+            if (i0 + k < rn) v[k] = *reinterpret_cast<const uint2 *>(p + (int64_t)(i0 + k) * ld);
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+            if (i0 + k < rn && !sk[i0 + k]) {
+                a02 += v[k].x & 0x00ff00ffu;
+                a13 += (v[k].x >> 8) & 0x00ff00ffu;
+                a46 += v[k].y & 0x00ff00ffu;
+                a57 += (v[k].y >> 8) & 0x00ff00ffu;
+            }
+        }
+    }
+    uint16_t *q = part + c * kColSegMax + seg;  // out[c] viewed as 4 x u16
+    const uint32_t s[8] = {a02 & 0xffffu, a13 & 0xffffu, a02 >> 16, a13 >> 16,
+                           a46 & 0xffffu, a57 & 0xffffu, a46 >> 16, a57 >> 16};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) q[j * kColSegMax] = (uint16_t)s[j];
+}
+
+__global__ void __launch_bounds__(256)
+colsum_u8_finish_kernel(double *__restrict__ out, int64_t ncols, int nseg, int64_t nrows,
+                        const uint8_t *__restrict__ skip)
+{
+    __shared__ int cnt[256];
+    int good = 0;
+    for (int64_t r = threadIdx.x; r < nrows; r += 256) good += (skip && skip[r]) ? 0 : 1;
+    cnt[threadIdx.x] = good;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) cnt[threadIdx.x] += cnt[threadIdx.x + off];
+        __syncthreads();
+    }
+    const double ngood = (double)cnt[0];
+    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c >= ncols) return;
+    const uint64_t w = reinterpret_cast<const uint64_t *>(out)[c];
+    uint32_t tot = 0;
+    for (int k = 0; k < nseg; ++k) tot += (uint32_t)((w >> (16 * k)) & 0xffffu);
+    out[c] = (double)tot / ngood;
+}
+
 __device__ __forceinline__ int64_t reflect_index(int64_t i, int64_t n)
 {
     // scipy 'reflect' (d c b a | a b c d | d c b a): period 2n, half-sample symmetric
@@ -926,6 +996,22 @@ int column_launches(int v, int64_t n, Launch &&launch)
 template <typename Tin>
 int col_means_t(const void *x, int64_t nrows, int64_t n, int64_t ld, const uint8_t *skip, double *out, hipStream_t s)
 {
+    if constexpr (sizeof(Tin) == 1) {
+        // 8-bit input: exact integer sums by row segments (PU_COLSEG=0: the sequential kernel)
+        static const bool seg = [] {
+            const char *e = getenv("PU_COLSEG");
+            return !e || atoi(e) != 0;
+        }();
+        const int nseg = (int)((nrows + kColSegRows - 1) / kColSegRows);
+        if (seg && nseg <= kColSegMax && n % 8 == 0 && ld % 8 == 0 && reinterpret_cast<uintptr_t>(x) % 8 == 0) {
+            hipLaunchKernelGGL(colsum_u8_seg_kernel, dim3(blocks_for(n / 8, 256), nseg), dim3(256), 0, s,
+                               reinterpret_cast<const uint8_t *>(x), nrows, n, ld, skip,
+                               reinterpret_cast<uint16_t *>(out));
+            hipLaunchKernelGGL(colsum_u8_finish_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, out, n, nseg,
+                               nrows, skip);
+            return PU_OK;
+        }
+    }
     const int v = pick_vec<Tin>(x, ld, vec_max(sizeof(Tin), 4));
     // bytes of rows in flight per lane and register buffer (PU_CLEAN_BATCH: 128 or 256)
     int bb = 256;  // C4 sweep (profiles/r02_clean/): f32 V=4 190 us vs 212 us at 128 B
