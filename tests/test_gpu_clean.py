@@ -210,3 +210,26 @@ def test_gaussian_filter1d_vs_scipy(gpu, n, sigma):
     _hip.check(lib.pu_gaussian_filter1d(_hip.ptr(xd), n, _hip.ptr(dw), radius, _hip.ptr(out), _hip.stream_ptr()),
                "pu_gaussian_filter1d")
     np.testing.assert_array_equal(out.cpu().numpy(), gaussian_filter1d(x, sigma, mode="reflect"))
+
+
+@pytest.mark.parametrize("nrows,ncols", [(300, 4096), (1024, 2048), (1, 64), (257, 8 * 1000)])
+def test_col_means_u8_segments(gpu, nrows, ncols):
+    """pu_col_means on 8-bit input takes the row-segment kernel (exact integer partial sums;
+    a partial last segment, skipped rows, a single row) and must equal the float64 mean over
+    the unskipped rows bit for bit."""
+    import torch
+    from pulsarutils import _hip
+    rng = np.random.default_rng(nrows * 7 + ncols)
+    x = rng.integers(0, 256, size=(nrows, ncols), dtype=np.uint8)
+    skip = (rng.random(nrows) < 0.2).astype(np.uint8)
+    if nrows > 1:
+        skip[0] = 1
+    xd, sd = torch.from_numpy(x).cuda(), torch.from_numpy(skip).cuda()
+    out = torch.empty(ncols, dtype=torch.float64, device="cuda")
+    lib = _hip.lib()
+    _hip.check(lib.pu_col_means(_hip.ptr(xd), _hip.dtype_code(xd.dtype), nrows, ncols, ncols, _hip.ptr(sd),
+                                _hip.ptr(out), _hip.stream_ptr()), "pu_col_means")
+    good = skip == 0
+    with np.errstate(invalid="ignore"):
+        ref = x[good].astype(np.float64).sum(axis=0) / float(good.sum())
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
