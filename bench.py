@@ -352,6 +352,7 @@ def main():
                 "roofline": roof, "clean": clean, "cpu_baseline": cpu}
         if bcast is not None:
             line["multi_gpu"] = bcast
+        line["build"] = _hip.build_info()  # was the library built from the sources shipped with it
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -68,6 +68,38 @@ class HipBackendError(RuntimeError):
     pass
 
 
+_SRC_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
+_INC_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "include")
+
+
+def source_hashes():
+    """SHA-256 of every source the library is built from (csrc/*.hip|cpp|h, include/*.h)."""
+    import hashlib
+    out = {}
+    for d, exts in ((_SRC_DIR, (".hip", ".cpp", ".h")), (_INC_DIR, (".h",))):
+        if not os.path.isdir(d):
+            continue
+        for name in sorted(os.listdir(d)):
+            if name.endswith(exts):
+                with open(os.path.join(d, name), "rb") as f:
+                    out[os.path.basename(d) + "/" + name] = hashlib.sha256(f.read()).hexdigest()
+    return out
+
+
+def build_info():
+    """Provenance of the library file: what ``__graft_entry__.build()`` recorded next to it
+    (source hashes, hipcc version, time) and whether the sources on disk still match -
+    False means the .so was built from other sources than the ones shipped beside it."""
+    import json
+    path = os.path.join(os.path.dirname(_LIB_PATH), "BUILD_INFO.json")
+    if not os.path.exists(path):
+        return {"recorded": False}
+    with open(path) as f:
+        rec = json.load(f)
+    return {"recorded": True, "built": rec.get("built"), "hipcc": rec.get("hipcc"),
+            "sources_match": rec.get("sources") == source_hashes()}
+
+
 def lib():
     """Load the HIP library (raises if it is missing: no silent fallback)."""
     global _lib
