@@ -1112,14 +1112,21 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
         if (dw >= 0) __builtin_amdgcn_s_setprio(1);
         if (active && !(a.skip & 2)) {
             const uint32_t sb = smem_addr + 8u * lane;  // window records: absolute LDS offsets
-            rec_t rec = rec0;
-            for (int g = st.x; g < st.y; ++g) {
-                rec_t next = g + 1 < st.y ? ld_uniform(recs + (size_t)(g + 1) * W) : rec;
-                group_trials<C>(acc2, rec, sb);
-                // the next record is consumed only here, after the group's last lgkmcnt(0):
-                // hoisted into the loop, its scalar-load wait drained the LDS read pipeline
-                asm volatile("" : "+s"(next));
-                rec = next;
+            // two groups per iteration with ping-pong records (no per-group record copy).
+            // A record is consumed only after the previous group's last lgkmcnt(0) (the empty
+            // asm): hoisted into the trial loop, its scalar-load wait drained the LDS reads.
+            // The row past the stage's last group is a valid record (clamped index): loaded,
+            // never used.
+            rec_t ra = rec0;
+            const int gl = st.y - 1;
+            for (int g = st.x; g < st.y; g += 2) {
+                rec_t rb = ld_uniform(recs + (size_t)min(g + 1, gl) * W);
+                group_trials<C>(acc2, ra, sb);
+                asm volatile("" : "+s"(rb));
+                if (g + 1 > gl) break;
+                ra = ld_uniform(recs + (size_t)min(g + 2, gl) * W);
+                group_trials<C>(acc2, rb, sb);
+                asm volatile("" : "+s"(ra));
             }
         }
         if (dw >= 0) __builtin_amdgcn_s_setprio(0);
