@@ -1013,7 +1013,7 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
         const uint32_t w1 = w0 + (uint32_t)copy_bytes - 4u;
         // M0 set twice per pass (copy 0, then copy 1) and not restored: hipcc sets M0 afresh
         // in the basic block of every LDS-DMA it emits (checked on the generated code by
-        // scripts/check_m0.py; the "m0" clobber is advisory - hipcc warns that M0 is
+        // scripts/check_m0.py; an "m0" clobber would be ignored - hipcc treats M0 as
         // reserved); nothing between these volatile statements uses M0.  (Saving and
         // restoring it cost two scalar instructions per pass: C2 15.78 vs 15.65 ms.)  Setting it around every
         // chunk's two stores instead cost ~7 scalar issue slots per chunk on the CU's shared
@@ -1021,14 +1021,12 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
         // spans whole passes (copy_bytes a multiple of 256 UP: C2's 2560 B at UP = 10) the
         // chunks past len only write the slot's own padding, so the stores need no guards.
         const bool whole = copy_bytes % (256 * UP) == 0;
-        // (M0 declared clobbered: the compiler re-materialises its own M0 before the next
-        // LDS-DMA, so no save / restore)
-        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(w0) : "memory", "m0");
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(w0) : "memory");
         if (whole) {
 #pragma unroll
             for (int u = 0; u < UP; ++u)
                 asm volatile("ds_write_addtid_b32 %0 offset:%1" : : "v"(r[u]), "i"(256 * u) : "memory");
-            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(w1) : "memory", "m0");
+            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(w1) : "memory");
 #pragma unroll
             for (int u = 0; u < UP; ++u)
                 asm volatile("ds_write_addtid_b32 %0 offset:%1" : : "v"(r[u]), "i"(256 * u) : "memory");
@@ -1037,7 +1035,7 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
             for (int u = 0; u < UP; ++u)
                 if (i0 + 64 * u < lim)
                     asm volatile("ds_write_addtid_b32 %0 offset:%1" : : "v"(r[u]), "i"(256 * u) : "memory");
-            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(w1) : "memory", "m0");
+            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(w1) : "memory");
 #pragma unroll
             for (int u = 0; u < UP; ++u)
                 if (i0 + 64 * u < lim)
