@@ -935,7 +935,10 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
         unsigned char *raw = smem + a.lds_bytes - ((nc * a.raw_stride * EB + 255) & ~255);
         const int cover_tile = (tile.z * EB + 255) & ~255;
         const uint32_t base_mask = (1u << a.base_bits) - 1u;
-        for (int k = kb; k < ke; ++k) {
+        // row pointers by increments (one 64-bit add per row instead of a 64-bit multiply)
+        const size_t row_step = (size_t)NDW * (size_t)o.ld;
+        const Tin *rowp = data + (size_t)(c0 + dw + NDW * kb) * (size_t)o.ld;
+        for (int k = kb; k < ke; ++k, rowp += row_step) {
             const int ci = dw + NDW * k;
             const int c = c0 + ci;
             // the row word: its base mod N and, in the top bits, this channel's own cover
@@ -946,12 +949,11 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
             int start = (int)(word & base_mask) + t0;
             if (start >= n) start -= n;
             if constexpr (EB == 4)
-                dma_row_f32(raw + ci * a.raw_stride * 4,
-                            reinterpret_cast<const float *>(data) + (size_t)c * (size_t)o.ld, start, cover_bytes, n,
+                dma_row_f32(raw + ci * a.raw_stride * 4, reinterpret_cast<const float *>(rowp), start, cover_bytes, n,
                             small_n, lane);
             else
-                dma_row_u8(raw + ci * a.raw_stride, reinterpret_cast<const unsigned char *>(data) + (size_t)c * (size_t)o.ld,
-                           start, cover_bytes, n, small_n, lane);
+                dma_row_u8(raw + ci * a.raw_stride, reinterpret_cast<const unsigned char *>(rowp), start, cover_bytes,
+                           n, small_n, lane);
         }
     };
 
