@@ -97,9 +97,34 @@ int pu_plan_search(pu_plan *plan, const void *data, int64_t ld, double *max_out,
  * records into the per-trial outputs exactly as pu_plan_search does. */
 int pu_plan_search_tiles(pu_plan *plan, const void *data, int64_t ld, int64_t tt_begin,
                          int64_t tt_end, void *workspace, size_t workspace_bytes, void *stream);
-int pu_plan_finalize(pu_plan *plan, double *max_out, double *std_out, double *snr_out,
-                     int32_t *rebin_out, const void *workspace, size_t workspace_bytes,
-                     void *stream);
+int pu_plan_finalize(pu_plan *plan, const void *data, int64_t ld, double *max_out,
+                     double *std_out, double *snr_out, int32_t *rebin_out, void *workspace,
+                     size_t workspace_bytes, void *stream);
+
+/* Certification (pu_plan_search and pu_plan_finalize).  The fast
+ * path's per-trial statistics are summed in another order than numpy's; a trial whose
+ * result that order could change - a zero or rounding-level std (constant input), a
+ * non-finite value, or (float64 accumulation, and uint8 input with exact float32 sums)
+ * two windows' S/N within the rounding bound of each other - is recomputed exactly:
+ * its series by float64 channel-order dedispersion (bit-identical to the reference's
+ * dedisperse) and its statistics by pu_series_stats.  An input holding NaN or +-inf
+ * gives every trial the reference's result max = std = NaN, snr = 0, rebin = 0.
+ * Both calls therefore synchronise ``stream`` once before returning (the outputs are
+ * final when they return).  pu_plan_info reports the trials of the last call that
+ * were recomputed ("cert_rechecked") and whether the NaN rule applied ("cert_nan"). */
+
+/* The reference's statistics of given float64 dedispersed series, in numpy's exact
+ * order (dedispersion.py:186-201, bit-exact): for each row r of series (rows x n,
+ * leading dimension ld) max = np.max(s), std = np.std(s) with s = row - np.mean(row),
+ * and the best S/N over the 1/2/4/8-sample rebinned s (quick_resample order) with the
+ * reference's strict first-best rule from (0, 0).  Outputs go to position index[r]
+ * (device int32; NULL = r).  workspace: 256-byte aligned; rows are processed in
+ * batches of as many as pu_series_stats_workspace_bytes(batch, n) <= workspace_bytes
+ * allows (at least one). */
+size_t pu_series_stats_workspace_bytes(int64_t rows, int64_t n);
+int pu_series_stats(const double *series, int64_t rows, int64_t n, int64_t ld,
+                    const int32_t *index, double *max_out, double *std_out, double *snr_out,
+                    int32_t *rebin_out, void *workspace, size_t workspace_bytes, void *stream);
 
 /* Replaces dedisperse (dedispersion.py:93-98) for every trial of the plan: writes
  * the dedispersed plane plane[trial * ld_plane + t] in the accumulation type
@@ -124,9 +149,10 @@ int pu_plan_stamps(pu_plan *plan, int64_t *out, int n);
 /* Introspection (tests / DESIGN.md): fills up to ``n`` of
  * {ndm, dm_tiles, time_tiles, trials_per_tile, time_tile, chans_per_step,
  *  row_stride, lds_bytes, acc_is_f64, max_spread, group, slots, stages,
- *  slot_bytes, raw_stride, exec_adds, lds_traffic}: the last two are the adds and
- *  LDS bytes (reads, writes, DMA) one launch executes (subband mode; 0 otherwise).
- *  Returns the count written. */
+ *  slot_bytes, raw_stride, exec_adds, lds_traffic, cert_rechecked, cert_nan}: exec_adds
+ *  and lds_traffic are the adds and LDS bytes (reads, writes, DMA) one launch executes
+ *  (subband mode; 0 otherwise); the last two describe the last search's certification
+ *  step (see pu_plan_finalize).  Returns the count written. */
 int pu_plan_info(const pu_plan *plan, int64_t *info, int n);
 
 /* ------------------------------------------------------------------ cleaning */

@@ -37,6 +37,7 @@
 #include <type_traits>
 #include <vector>
 
+#include "exact.h"
 #include "pu_common.h"
 
 namespace {
@@ -1183,19 +1184,48 @@ dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__res
                                             pu::xcd_remap(blockIdx.x, gridDim.x), true);
 }
 
+// Certification state at the workspace tail (pu_plan_workspace_bytes), then the list
+// of the trials to recompute (int32 each).
+struct CertState {
+    int32_t nflag;       // trials the fast path could not certify (listed after the state)
+    int32_t nnonfinite;  // of which: a non-finite partial (NaN / inf in the series)
+    int32_t scan;        // non-finite input scan (pu::nonfinite_any_async)
+    int32_t pad[61];
+};
+static_assert(sizeof(CertState) == 256, "CertState");
+
+// Rounding model of one plan's fast statistics.
+struct CertModel {
+    int32_t tie_check;  // the series is exact (u8 with exact f32 sums, any f64 accumulation)
+    double e_rel;       // per-sample series error bound / (|mean| + 4 std + |max|)
+    double gamma;       // relative rounding of the epilogue's sums of (shifted) squares
+};
+
 // One workgroup per trial: combine the per-time-tile partials in a fixed order
 // (thread-strided then an LDS tree: deterministic), then the reference's S/N logic
 // (dedispersion.py:186-201): snr_w = max(reb_w)/std(reb_w), first strict best.
+// Certification: a trial whose statistics or S/N decisions the fast path's summation
+// order could change is appended to the list in ``cert`` (the host recomputes it
+// exactly).  Bounds: the epilogue's sums of squares carry relative error gamma of
+// Q = their magnitude (tile-local second moments + recentring terms), so
+// |d var| <= 4 gamma Q; a per-sample series error E moves a width-w std by <= w E and
+// max - w mean by <= 2 w E.  A trial is flagged when a partial is non-finite, when
+// std is not > 4 x its bound (zero or rounding-level std: constant inputs), when
+// max - w mean is within its bound of 0 (the S/N sign decision), and - for plans whose
+// series is exact - when two S/N values of the strict first-best chain are within the
+// sum of their bounds (ties).
 __global__ void __launch_bounds__(256)
 pu_finalize_kernel(const double *__restrict__ part, int ntt, int n, int tt_len,
-                   double *max_out, double *std_out, double *snr_out, int32_t *win_out)
+                   double *max_out, double *std_out, double *snr_out, int32_t *win_out,
+                   CertModel cm, CertState *cert, int32_t *list)
 {
-    __shared__ double red[3][4][256];
+    __shared__ double red[4][4][256];
     const int trial = blockIdx.x;
     const int tid = threadIdx.x;
     const double *p = part + (size_t)trial * ntt * kPartStride;
     const double mu = p[0];
     double S1[4] = {0, 0, 0, 0}, S2[4] = {0, 0, 0, 0}, MX[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    double A2[4] = {0, 0, 0, 0};
     for (int i = tid; i < ntt; i += 256) {
         const double *q = p + (size_t)i * kPartStride;
         const double dk = q[0] - mu;
@@ -1209,13 +1239,16 @@ pu_finalize_kernel(const double *__restrict__ part, int ntt, int n, int tt_len,
             const double wd = width * dk;
             S1[w] += s1 + cntb * wd;
             S2[w] += s2 + 2.0 * wd * s1 + cntb * wd * wd;
-            MX[w] = fmax(MX[w], q[1 + 3 * w]);
+            A2[w] += fabs(s2) + cntb * wd * wd;
+            // NaN-propagating (a NaN partial max makes the trial non-finite below)
+            MX[w] = (q[1 + 3 * w] > MX[w] || q[1 + 3 * w] != q[1 + 3 * w]) ? q[1 + 3 * w] : MX[w];
         }
     }
     for (int w = 0; w < 4; ++w) {
         red[0][w][tid] = S1[w];
         red[1][w][tid] = S2[w];
         red[2][w][tid] = MX[w];
+        red[3][w][tid] = A2[w];
     }
     __syncthreads();
     for (int s = 128; s > 0; s >>= 1) {
@@ -1223,7 +1256,9 @@ pu_finalize_kernel(const double *__restrict__ part, int ntt, int n, int tt_len,
             for (int w = 0; w < 4; ++w) {
                 red[0][w][tid] += red[0][w][tid + s];
                 red[1][w][tid] += red[1][w][tid + s];
-                red[2][w][tid] = fmax(red[2][w][tid], red[2][w][tid + s]);
+                const double a = red[2][w][tid], b = red[2][w][tid + s];
+                red[2][w][tid] = (b > a || b != b) ? b : a;
+                red[3][w][tid] += red[3][w][tid + s];
             }
         }
         __syncthreads();
@@ -1232,7 +1267,8 @@ pu_finalize_kernel(const double *__restrict__ part, int ntt, int n, int tt_len,
         const double mean = mu + red[0][0][0] / n;  // mean of the dedispersed series
         double best = 0.0;
         int bestw = 0;
-        double sd1 = 0.0;
+        double sdw[4] = {0, 0, 0, 0}, Qw[4] = {0, 0, 0, 0};
+        bool nonfinite = !isfinite(mu) || !isfinite(mean);
         for (int w = 0; w < 4; ++w) {
             const int width = 1 << w;
             const long nb = n / width;
@@ -1240,15 +1276,51 @@ pu_finalize_kernel(const double *__restrict__ part, int ntt, int n, int tt_len,
             const double m1 = red[0][w][0] / nb;
             const double var = red[1][w][0] / nb - m1 * m1;
             const double sd = sqrt(var > 0 ? var : 0.0);
-            if (w == 0) sd1 = sd;
+            sdw[w] = sd;
+            Qw[w] = red[3][w][0] / nb;
+            nonfinite = nonfinite || !isfinite(red[0][w][0]) || !isfinite(red[1][w][0]) ||
+                        !isfinite(red[2][w][0]) || !isfinite(red[3][w][0]);
             const double snr = (red[2][w][0] - width * mean) / sd;
             if (snr > best) {
                 best = snr;
                 bestw = width;
             }
         }
+        bool uncertain = false;
+        if (!nonfinite) {
+            const double E = cm.e_rel * (fabs(mean) + 4.0 * sdw[0] + fabs(red[2][0][0]));
+            double b = 0.0, eb = 0.0;  // the reference's (best_snr, its bound) chain
+            for (int w = 0; w < 4 && !uncertain; ++w) {
+                const int width = 1 << w;
+                if (n / width <= 0) continue;
+                const double sd = sdw[w], MXw = red[2][w][0];
+                const double e_var = 4.0 * cm.gamma * Qw[w];
+                const double e_sd = sd > 0 ? e_var / sd + width * E : INFINITY;
+                const double num = MXw - width * mean;
+                const double e_num = 2.0 * width * E + cm.gamma * (fabs(MXw) + width * sqrt(Qw[0])) +
+                                     0x1p-50 * (fabs(MXw) + width * fabs(mean));
+                if (!(e_sd <= 0.25 * sd) || !(fabs(num) > e_num)) {
+                    uncertain = true;
+                    break;
+                }
+                const double snr = num / sd;
+                const double e_snr = (e_num + fabs(snr) * e_sd) / (sd - e_sd) + 0x1p-44 * fabs(snr);
+                if (cm.tie_check) {
+                    const double d = snr - b;
+                    if (!(fabs(d) > e_snr + eb)) uncertain = true;
+                    else if (d > 0) {
+                        b = snr;
+                        eb = e_snr;
+                    }
+                }
+            }
+        }
+        if (nonfinite || uncertain) {
+            list[atomicAdd(&cert->nflag, 1)] = trial;
+            if (nonfinite) atomicAdd(&cert->nnonfinite, 1);
+        }
         max_out[trial] = red[2][0][0] - mean;
-        std_out[trial] = sd1;
+        std_out[trial] = sdw[0];
         snr_out[trial] = best;
         win_out[trial] = bestw;
     }
@@ -1317,6 +1389,11 @@ struct pu_plan {
     std::vector<hipEvent_t> ev_start, ev_stop;
     int64_t launches = 0;
     uint64_t *d_stamps = nullptr;  // diagnostic build (PU_STAMPS): phase-cycle totals
+    // certification: the shift table (host) for exact recomputation of
+    // flagged trials, a pinned copy of the device CertState, the last call's outcome
+    std::vector<int64_t> shifts;
+    CertState *h_cert = nullptr;
+    int64_t cert_rechecked = 0, cert_nan = 0;
 };
 
 namespace {
@@ -1463,6 +1540,7 @@ void free_plan(pu_plan *p)
     (void)hipFree(p->d_slots);
     (void)hipFree(p->d_recs);
     (void)hipFree(p->d_stamps);
+    if (p->h_cert) (void)hipHostFree(p->h_cert);
     delete p;
 }
 
@@ -1950,6 +2028,122 @@ void reset_tables(pu_plan *p)
     *p = keep;
 }
 
+// The plan keeps its shift table (host) for the exact recomputation of flagged trials,
+// and a pinned copy of the certification state.
+int finish_plan(pu_plan *p, const int64_t *shifts)
+{
+    p->shifts.assign(shifts, shifts + p->ndm * p->nchan);
+    return pu::hip_check(hipHostMalloc((void **)&p->h_cert, sizeof(CertState), hipHostMallocDefault),
+                         "hipHostMalloc(cert)");
+}
+
+size_t part_bytes(const pu_plan *p) { return ((size_t)p->ndm * p->ntt * kPartStride * sizeof(double) + 255) & ~size_t(255); }
+
+// Rounding model of the plan's fast statistics (pu_finalize_kernel).
+CertModel cert_model(const pu_plan *p)
+{
+    CertModel m{};
+    if (kVariants[p->variant].acc_f64) {
+        m.tie_check = 1;  // float64 channel order: the reference's series bit for bit
+        m.e_rel = 0x1p-50;
+        m.gamma = 0x1p-44;
+    } else if (p->dtype == PU_U8 && 8 * 255 * p->nchan < (int64_t(1) << 24)) {
+        m.tie_check = 1;  // integer sums (and their 8-sample rebins) below 2^24: exact in float32
+        m.e_rel = 0.0;
+        m.gamma = 0x1p-19;
+    } else {
+        // float32 sums of float data: the typical (random-walk) rounding of nchan terms
+        // with an 8x margin, relative to the series' magnitude; S/N ties within the
+        // float32 tolerance are not recomputed (the stated tolerance covers them)
+        m.tie_check = 0;
+        m.e_rel = 8.0 * 0x1p-24 * std::sqrt((double)p->nchan);
+        m.gamma = 0x1p-19;
+    }
+    return m;
+}
+
+int launch_finalize(pu_plan *p, const double *part, double *mx, double *sd, double *snr, int32_t *win, char *ws,
+                    hipStream_t s)
+{
+    CertState *cert = reinterpret_cast<CertState *>(ws + part_bytes(p));
+    int32_t *list = reinterpret_cast<int32_t *>(cert + 1);
+    PU_TRY_HIP(hipMemsetAsync(cert, 0, sizeof(CertState), s));
+    hipLaunchKernelGGL(pu_finalize_kernel, dim3((unsigned)p->ndm), dim3(256), 0, s, part, p->ntt, (int)p->n, p->TT,
+                       mx, sd, snr, win, cert_model(p), cert, list);
+    return pu::launch_check("pu_finalize_kernel");
+}
+
+// After the finalize kernel: wait for it, then settle the flagged trials.  An input
+// holding NaN / inf (found by a scan, run only when some trial saw a non-finite value)
+// gives every trial the reference's NaN result; other flagged trials are recomputed
+// exactly - float64 channel-order dedispersion (a channel-mode sub-plan of the flagged
+// trials' shifts: the reference's series bit for bit) + pu_series_stats - in batches
+// that fit ~1 GiB of scratch.
+int resolve_flagged(pu_plan *p, const void *data, int64_t ld, double *mx, double *sd, double *snr, int32_t *win,
+                    char *ws, hipStream_t s)
+{
+    CertState *cert = reinterpret_cast<CertState *>(ws + part_bytes(p));
+    const int32_t *list = reinterpret_cast<const int32_t *>(cert + 1);
+    p->cert_rechecked = 0;
+    p->cert_nan = 0;
+    PU_TRY_HIP(hipMemcpyAsync(p->h_cert, cert, sizeof(CertState), hipMemcpyDeviceToHost, s));
+    PU_TRY_HIP(hipStreamSynchronize(s));
+    const int64_t nflag = p->h_cert->nflag;
+    if (nflag == 0) return PU_OK;
+    if (p->h_cert->nnonfinite > 0 && p->dtype != PU_U8) {
+        int rc = pu::nonfinite_any_async(data, p->dtype, p->nchan, p->n, ld, &cert->scan, s);
+        if (rc) return rc;
+        PU_TRY_HIP(hipMemcpyAsync(p->h_cert, cert, sizeof(CertState), hipMemcpyDeviceToHost, s));
+        PU_TRY_HIP(hipStreamSynchronize(s));
+        if (p->h_cert->scan) {
+            // every trial's series holds every input sample once (circular shift-and-sum),
+            // so a NaN / inf anywhere reaches every trial: np.mean -> NaN or inf, the
+            // shifted series -> NaN, max = std = NaN, no S/N beats 0 (dedispersion.py:186-201)
+            p->cert_nan = 1;
+            int rc2 = pu::nan_rule(p->ndm, mx, sd, snr, win, s);
+            if (rc2) return rc2;
+            PU_TRY_HIP(hipStreamSynchronize(s));
+            return PU_OK;
+        }
+    }
+    std::vector<int32_t> idx((size_t)nflag);
+    PU_TRY_HIP(hipMemcpyAsync(idx.data(), list, (size_t)nflag * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    PU_TRY_HIP(hipStreamSynchronize(s));
+    std::sort(idx.begin(), idx.end());
+    const int64_t n = p->n, nchan = p->nchan;
+    const int64_t per_row = n * 8 + (int64_t)pu_series_stats_workspace_bytes(1, n);
+    const int64_t B = std::max<int64_t>(1, std::min<int64_t>(nflag, (int64_t(1) << 30) / per_row));
+    double *plane = nullptr;
+    void *sws = nullptr;
+    int32_t *d_idx = nullptr;
+    const size_t sws_bytes = pu_series_stats_workspace_bytes(B, n);
+    int rc = pu::hip_check(hipMalloc((void **)&plane, (size_t)B * n * sizeof(double)), "hipMalloc(recheck plane)");
+    if (!rc) rc = pu::hip_check(hipMalloc(&sws, sws_bytes), "hipMalloc(recheck workspace)");
+    if (!rc) rc = pu::hip_check(hipMalloc((void **)&d_idx, (size_t)B * sizeof(int32_t)), "hipMalloc(recheck index)");
+    std::vector<int64_t> sh;
+    for (int64_t i0 = 0; !rc && i0 < nflag; i0 += B) {
+        const int64_t m = std::min(B, nflag - i0);
+        sh.resize((size_t)(m * nchan));
+        for (int64_t k = 0; k < m; ++k)
+            std::copy_n(p->shifts.data() + (size_t)idx[(size_t)(i0 + k)] * nchan, nchan, sh.data() + k * nchan);
+        pu_plan *q = nullptr;
+        rc = pu_plan_create_grouped(&q, p->dtype, PU_ACC_F64, nchan, n, sh.data(), m, 1);
+        if (!rc) rc = pu_plan_dedisperse(q, data, ld, plane, n, s);
+        if (!rc)
+            rc = pu::hip_check(hipMemcpyAsync(d_idx, idx.data() + i0, (size_t)m * sizeof(int32_t),
+                                              hipMemcpyHostToDevice, s), "hipMemcpyAsync(recheck index)");
+        if (!rc) rc = pu_series_stats(plane, m, n, n, d_idx, mx, sd, snr, win, sws, sws_bytes, s);
+        const int rs = pu::hip_check(hipStreamSynchronize(s), "hipStreamSynchronize(recheck)");
+        if (!rc) rc = rs;
+        if (q) pu_plan_destroy(q);
+    }
+    (void)hipFree(plane);
+    (void)hipFree(sws);
+    (void)hipFree(d_idx);
+    if (!rc) p->cert_rechecked = nflag;
+    return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2045,6 +2239,7 @@ int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int
         }
         if (keep) {
             rc = upload_sub(keep);
+            if (!rc) rc = finish_plan(keep, shifts);
             if (rc) {
                 free_plan(keep);
                 return rc;
@@ -2062,6 +2257,7 @@ int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int
         if (rc == PU_EUNSUPPORTED) reset_tables(p);
     }
     if (rc == PU_EUNSUPPORTED) rc = plan_channels(p, shifts, budget);
+    if (!rc) rc = finish_plan(p, shifts);
     if (rc) {
         free_plan(p);
         return rc;
@@ -2126,7 +2322,8 @@ int pu_plan_kernel_times(pu_plan *p, float *ms, int n)
 size_t pu_plan_workspace_bytes(const pu_plan *p)
 {
     if (!p) return 0;
-    return (size_t)p->ndm * p->ntt * kPartStride * sizeof(double);
+    // per-(trial, time tile) partial records | CertState | flagged-trial list
+    return part_bytes(p) + sizeof(CertState) + (size_t)p->ndm * sizeof(int32_t);
 }
 
 int pu_plan_info(const pu_plan *p, int64_t *info, int n)
@@ -2135,7 +2332,7 @@ int pu_plan_info(const pu_plan *p, int64_t *info, int n)
     const int64_t v[] = {p->ndm, p->ndt, p->ntt, p->group > 1 ? with_shape(p->shape, [](auto c) { return decltype(c)::T; }) : kTPT, p->TT, p->ncc,
                          p->row_stride, (int64_t)p->lds_bytes, kVariants[p->variant].acc_f64, p->max_spread,
                          p->group, p->nslots_total, p->nstages, (int64_t)p->slot_bytes, p->raw_stride,
-                         p->exec_adds, p->lds_traffic};
+                         p->exec_adds, p->lds_traffic, p->cert_rechecked, p->cert_nan};
     const int m = std::min<int>(n, (int)(sizeof v / sizeof v[0]));
     for (int k = 0; k < m; ++k) info[k] = v[k];
     return m;
@@ -2185,16 +2382,19 @@ int pu_plan_search_tiles(pu_plan *p, const void *data, int64_t ld, int64_t tt_be
     return dispatch(p, a, false, pu::as_stream(stream));
 }
 
-int pu_plan_finalize(pu_plan *p, double *max_out, double *std_out, double *snr_out, int32_t *rebin_out,
-                     const void *workspace, size_t ws_bytes, void *stream)
+int pu_plan_finalize(pu_plan *p, const void *data, int64_t ld, double *max_out, double *std_out, double *snr_out,
+                     int32_t *rebin_out, void *workspace, size_t ws_bytes, void *stream)
 {
-    PU_REQUIRE(p != nullptr, "plan is NULL");
+    int rc = check_data(p, data, ld);
+    if (rc) return rc;
     PU_REQUIRE(max_out && std_out && snr_out && rebin_out, "pu_plan_finalize: NULL output");
-    PU_REQUIRE(workspace && ws_bytes >= pu_plan_workspace_bytes(p), "pu_plan_finalize: workspace too small");
-    hipLaunchKernelGGL(pu_finalize_kernel, dim3((unsigned)p->ndm), dim3(256), 0, pu::as_stream(stream),
-                       reinterpret_cast<const double *>(workspace), p->ntt, (int)p->n, p->TT, max_out, std_out,
-                       snr_out, rebin_out);
-    return pu::launch_check("pu_finalize_kernel");
+    PU_REQUIRE(workspace && ws_bytes >= pu_plan_workspace_bytes(p) && reinterpret_cast<uintptr_t>(workspace) % 8 == 0,
+               "pu_plan_finalize: workspace too small or not 8-byte aligned");
+    hipStream_t s = pu::as_stream(stream);
+    char *ws = reinterpret_cast<char *>(workspace);
+    rc = launch_finalize(p, reinterpret_cast<const double *>(ws), max_out, std_out, snr_out, rebin_out, ws, s);
+    if (rc) return rc;
+    return resolve_flagged(p, data, ld, max_out, std_out, snr_out, rebin_out, ws, s);
 }
 
 int pu_plan_search(pu_plan *p, const void *data, int64_t ld, double *max_out, double *std_out,
@@ -2203,15 +2403,17 @@ int pu_plan_search(pu_plan *p, const void *data, int64_t ld, double *max_out, do
     int rc = check_data(p, data, ld);
     if (rc) return rc;
     PU_REQUIRE(max_out && std_out && snr_out && rebin_out, "pu_plan_search: NULL output");
-    PU_REQUIRE(workspace && ws_bytes >= pu_plan_workspace_bytes(p), "pu_plan_search: workspace too small");
+    PU_REQUIRE(workspace && ws_bytes >= pu_plan_workspace_bytes(p) && reinterpret_cast<uintptr_t>(workspace) % 8 == 0,
+               "pu_plan_search: workspace too small or not 8-byte aligned");
     DedispArgs a = make_args(p, data, ld);
     a.partials = reinterpret_cast<double *>(workspace);
     hipStream_t s = pu::as_stream(stream);
     rc = dispatch(p, a, false, s);
     if (rc) return rc;
-    hipLaunchKernelGGL(pu_finalize_kernel, dim3((unsigned)p->ndm), dim3(256), 0, s, a.partials, p->ntt,
-                       (int)p->n, p->TT, max_out, std_out, snr_out, rebin_out);
-    return pu::launch_check("pu_finalize_kernel");
+    char *ws = reinterpret_cast<char *>(workspace);
+    rc = launch_finalize(p, a.partials, max_out, std_out, snr_out, rebin_out, ws, s);
+    if (rc) return rc;
+    return resolve_flagged(p, data, ld, max_out, std_out, snr_out, rebin_out, ws, s);
 }
 
 int pu_plan_dedisperse(pu_plan *p, const void *data, int64_t ld, void *plane, int64_t ld_plane, void *stream)

@@ -34,7 +34,9 @@ SIGNATURES = {
     "pu_plan_search": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "pu_plan_dedisperse": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp]),
     "pu_plan_search_tiles": (_i32, [_vp, _vp, _i64, _i64, _i64, _vp, _sz, _vp]),
-    "pu_plan_finalize": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "pu_plan_finalize": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "pu_series_stats_workspace_bytes": (_sz, [_i64, _i64]),
+    "pu_series_stats": (_i32, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "pu_plan_info": (_i32, [_vp, _vp, _i32]),
     "pu_plan_enable_timing": (_i32, [_vp, _i32]),
     "pu_plan_kernel_times": (_i32, [_vp, _vp, _i32]),
@@ -61,7 +63,7 @@ SIGNATURES = {
 
 INFO_FIELDS = ("ndm", "dm_tiles", "time_tiles", "trials_per_tile", "time_tile", "chans_per_step",
                "row_stride", "lds_bytes", "acc_is_f64", "max_spread", "group", "slots", "stages",
-               "slot_bytes", "raw_stride", "exec_adds", "lds_traffic")
+               "slot_bytes", "raw_stride", "exec_adds", "lds_traffic", "cert_rechecked", "cert_nan")
 
 
 class HipBackendError(RuntimeError):
@@ -242,64 +244,81 @@ class Plan:
             raise ValueError(f"data dtype {data.dtype} does not match the plan's dtype code {self.dtype_code}")
 
     @staticmethod
-    def _rows_aligned(data):
+    def _rows_aligned(data, stream=None):
         """8-bit rows are staged by LDS-DMA in whole dwords: a view whose rows do not start
-        on 4-byte boundaries is copied once into a fresh (aligned, contiguous) tensor."""
+        on 4-byte boundaries is copied once into a fresh (aligned, contiguous) tensor.  The
+        copy is made ON the launch stream (so it is ordered after whatever that stream
+        waits for, and the caching allocator only reuses its memory after that stream's
+        later work, i.e. after the kernel that reads it)."""
         if data.element_size() == 1 and (data.data_ptr() % 4 or data.stride(0) % 4):
-            return data.clone(memory_format=torch().contiguous_format)
+            t = torch()
+            with t.cuda.stream(stream if stream is not None else t.cuda.current_stream(data.device)):
+                return data.clone(memory_format=t.contiguous_format)
         return data
 
-    def search(self, data, out=None, workspace=None, stream=None):
-        """Launch the fused search; returns (max, std, snr, rebin) device tensors."""
+    def _outs_ws(self, dev, out, workspace):
+        """Output tensors and workspace of a search / finalize: allocated when None,
+        validated otherwise (dtype, length, contiguity, device, size) before any launch
+        writes them."""
         t = torch()
-        self._check_data(data)
-        data = self._rows_aligned(data)
-        dev = data.device
+        want = (t.float64, t.float64, t.float64, t.int32)
         if out is None:
-            out = (t.empty(self.ndm, dtype=t.float64, device=dev), t.empty(self.ndm, dtype=t.float64, device=dev),
-                   t.empty(self.ndm, dtype=t.float64, device=dev), t.empty(self.ndm, dtype=t.int32, device=dev))
-        else:
-            want = (t.float64, t.float64, t.float64, t.int32)
-            if len(out) != 4 or any(o.dtype != w or o.numel() < self.ndm or not o.is_contiguous() or o.device != dev
-                                    for o, w in zip(out, want)):
-                raise ValueError(f"out must be 3 float64 + 1 int32 contiguous tensors of >= {self.ndm} "
-                                 f"elements on {dev}")
+            out = tuple(t.empty(self.ndm, dtype=w, device=dev) for w in want)
+        elif len(out) != 4 or any(not isinstance(o, t.Tensor) or o.dtype != w or o.numel() < self.ndm
+                                  or not o.is_contiguous() or o.device != dev for o, w in zip(out, want)):
+            raise ValueError(f"out must be 3 float64 + 1 int32 contiguous tensors of >= {self.ndm} "
+                             f"elements on {dev}")
         if workspace is None:
             workspace = t.empty(max(self.workspace_bytes, 16), dtype=t.uint8, device=dev)
-        elif workspace.device != dev or not workspace.is_contiguous():
-            raise ValueError("workspace must be a contiguous tensor on the data's device")
+        elif (not isinstance(workspace, t.Tensor) or workspace.device != dev or not workspace.is_contiguous()
+              or workspace.numel() * workspace.element_size() < self.workspace_bytes
+              or workspace.data_ptr() % 8):
+            raise ValueError(f"workspace must be a contiguous, 8-byte aligned tensor of >= "
+                             f"{self.workspace_bytes} bytes on {dev}")
+        return out, workspace
+
+    def search(self, data, out=None, workspace=None, stream=None):
+        """Launch the fused search (+ certification); returns (max, std,
+        snr, rebin) device tensors, final when this returns."""
+        self._check_data(data)
+        data = self._rows_aligned(data, stream)
+        out, workspace = self._outs_ws(data.device, out, workspace)
         check(lib().pu_plan_search(self._h, ptr(data), data.stride(0), ptr(out[0]), ptr(out[1]), ptr(out[2]),
-                                   ptr(out[3]), ptr(workspace), workspace.numel(), stream_ptr(stream)),
+                                   ptr(out[3]), ptr(workspace), workspace.numel() * workspace.element_size(),
+                                   stream_ptr(stream)),
               "pu_plan_search")
         return out
-
-    def _outs_ws(self, dev, out, workspace):
-        t = torch()
-        if out is None:
-            out = (t.empty(self.ndm, dtype=t.float64, device=dev), t.empty(self.ndm, dtype=t.float64, device=dev),
-                   t.empty(self.ndm, dtype=t.float64, device=dev), t.empty(self.ndm, dtype=t.int32, device=dev))
-        if workspace is None:
-            workspace = t.empty(max(self.workspace_bytes, 16), dtype=t.uint8, device=dev)
-        if workspace.numel() < self.workspace_bytes or workspace.device != dev:
-            raise ValueError(f"workspace must hold {self.workspace_bytes} bytes on {dev}")
-        return out, workspace
 
     def search_tiles(self, data, tt_begin, tt_end, workspace, stream=None):
         """Shift-and-sum + per-tile statistics of time tiles [tt_begin, tt_end) only
         (pu_plan_search_tiles); ``finalize`` after every tile has run."""
         self._check_data(data)
-        data = self._rows_aligned(data)
-        _, workspace = self._outs_ws(data.device, (), workspace)
+        data = self._rows_aligned(data, stream)
+        _, workspace = self._outs_ws(data.device, None, workspace)
         check(lib().pu_plan_search_tiles(self._h, ptr(data), data.stride(0), int(tt_begin), int(tt_end),
-                                         ptr(workspace), workspace.numel(), stream_ptr(stream)),
+                                         ptr(workspace), workspace.numel() * workspace.element_size(),
+                                         stream_ptr(stream)),
               "pu_plan_search_tiles")
 
-    def finalize(self, workspace, out=None, stream=None):
-        """Per-trial (max, std, snr, rebin) from the per-tile records (pu_plan_finalize)."""
-        out, workspace = self._outs_ws(workspace.device, out, workspace)
-        check(lib().pu_plan_finalize(self._h, ptr(out[0]), ptr(out[1]), ptr(out[2]), ptr(out[3]), ptr(workspace),
-                                     workspace.numel(), stream_ptr(stream)), "pu_plan_finalize")
+    def finalize(self, workspace, data, out=None, stream=None):
+        """Per-trial (max, std, snr, rebin) from the per-tile records (pu_plan_finalize);
+        ``data`` is the searched filterbank (trials the fast statistics cannot certify
+        are recomputed from it exactly)."""
+        self._check_data(data)
+        data = self._rows_aligned(data, stream)
+        out, workspace = self._outs_ws(data.device, out, workspace)
+        check(lib().pu_plan_finalize(self._h, ptr(data), data.stride(0), ptr(out[0]), ptr(out[1]), ptr(out[2]),
+                                     ptr(out[3]), ptr(workspace), workspace.numel() * workspace.element_size(),
+                                     stream_ptr(stream)), "pu_plan_finalize")
         return out
+
+    def cert_info(self):
+        """Certification outcome of the last search / finalize: trials recomputed exactly
+        and whether the input's NaN / inf rule applied."""
+        info = np.zeros(len(INFO_FIELDS), np.int64)
+        lib().pu_plan_info(self._h, info.ctypes.data_as(ctypes.c_void_p), len(INFO_FIELDS))
+        d = dict(zip(INFO_FIELDS, info.tolist()))
+        return {"rechecked": d["cert_rechecked"], "nan_rule": bool(d["cert_nan"])}
 
     def tile_window(self, tt):
         """Half-open sample range [a, b) (NOT reduced mod nsamples) time tile ``tt``
@@ -325,7 +344,7 @@ class Plan:
         """Dedispersed plane (ndm, nsamples) in the accumulation dtype."""
         t = torch()
         self._check_data(data)
-        data = self._rows_aligned(data)
+        data = self._rows_aligned(data, stream)
         pdt = t.float64 if self.acc_is_f64 else t.float32
         if plane is None:
             plane = t.empty((self.ndm, self.nsamples), dtype=pdt, device=data.device)
@@ -344,4 +363,27 @@ def shift_table(nchan, trial_dms, start_freq, bandwidth, sample_time):
     check(lib().pu_shift_table(int(nchan), dms.ctypes.data_as(ctypes.c_void_p), dms.size, float(start_freq),
                                float(bandwidth), float(sample_time), out.ctypes.data_as(ctypes.c_void_p)),
           "pu_shift_table")
+    return out
+
+
+def series_stats(series, stream=None):
+    """pu_series_stats: the reference's per-trial (max, std, snr, rebin) of float64
+    dedispersed series (rows of a 2-D CUDA tensor), in numpy's exact order."""
+    t = require_gpu()
+    if not (isinstance(series, t.Tensor) and series.is_cuda and series.dtype == t.float64 and series.dim() == 2
+            and series.stride(1) == 1):
+        raise ValueError("series must be a 2-D row-major float64 CUDA tensor")
+    rows, n = series.shape
+    dev = series.device
+    out = (t.empty(rows, dtype=t.float64, device=dev), t.empty(rows, dtype=t.float64, device=dev),
+           t.empty(rows, dtype=t.float64, device=dev), t.empty(rows, dtype=t.int32, device=dev))
+    if rows == 0:
+        return out
+    per = max(1, min(rows, (1 << 30) // max(1, 12 * n)))
+    wsb = lib().pu_series_stats_workspace_bytes(per, n)
+    ws = t.empty(wsb + 256, dtype=t.uint8, device=dev)
+    off = (-ws.data_ptr()) % 256
+    check(lib().pu_series_stats(ptr(series), rows, n, series.stride(0), None, ptr(out[0]), ptr(out[1]), ptr(out[2]),
+                                ptr(out[3]), ctypes.c_void_p(ws.data_ptr() + off), wsb, stream_ptr(stream)),
+          "pu_series_stats")
     return out

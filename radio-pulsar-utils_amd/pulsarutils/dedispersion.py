@@ -173,6 +173,11 @@ def search_device(data, trial_DMs, nchan, start_freq, bandwidth, sample_time, ac
     x = _prepare_data(data)
     if int(nchan) != x.shape[0]:
         raise ValueError("nchan does not match data.shape[0]")
+    if x.shape[1] < 8:
+        # the reference's 8-sample quick_resample is empty and np.max of it raises
+        # (dedispersion.py:192-193)
+        raise ValueError("zero-size array to reduction operation maximum which has no identity "
+                         f"(nsamples {x.shape[1]} < 8)")
     if plan is None:
         dms = np.ascontiguousarray(np.atleast_1d(np.asarray(trial_DMs, dtype=np.float64)))
         ident = ("dm", hashlib.sha1(dms.tobytes()).hexdigest(), dms.size, float(start_freq),

@@ -116,7 +116,7 @@ def pipelined_broadcast_search(data, plan, out=None, workspace=None, src=0, chun
         return None
     if not done.all():
         raise RuntimeError("pipelined search: time tiles left unsearched")
-    plan.finalize(workspace, out=out, stream=comp)
+    plan.finalize(workspace, data, out=out, stream=comp)
     for o in out:
         o.record_stream(comp)
     cur.wait_stream(comp)

@@ -260,6 +260,68 @@ if not have("fil_u8_badchans"):
         meta[f"fil_{dt}_badchans_txt"] = open(fname + ".badchans").read()
     log("file statistics goldens")
 
+# ---------------------------------------------------------------- degenerate trials (dedispersion.py:186-201)
+# All-zero, constant, NaN/inf-carrying and S/N-tie inputs (tests/degenerate_cases.py).
+# The small cases run the reference's ``_dedispersion_search`` as it is.  The C1- and
+# C2-shaped cases (too slow for the interpreted roll_and_sum loop: 1e9 Python
+# iterations per C2 trial) run it with the module's ``dedisperse`` replaced by a
+# vectorised equivalent that adds the same float64 values in the same channel order
+# (``s += np.roll(row, normalize_shifts(-shifts, N)[c])``, the reference's own
+# normalize_shifts); the replacement is checked bit-for-bit against the reference's
+# dedisperse on every small case first.  Everything else (mean, quick_resample,
+# np.max / np.std, the strict ``snr > best_snr`` rule) is the reference's code.
+import degenerate_cases as DC  # noqa: E402
+
+_orig_dedisperse = D.dedisperse
+
+
+def _vec_dedisperse(data, shifts):
+    N = data.shape[1]
+    sh = D.normalize_shifts(-shifts, N)
+    s = np.zeros(N)
+    for c in range(data.shape[0]):
+        s += np.roll(data[c], int(sh[c]))
+    return s
+
+
+def _deg_run(case, patched):
+    nchan, f0, bw, ts = DC.band(case)
+    x = DC.make(case)
+    dms = DC.trial_dms(case.split(":")[0])
+    if dms is None:
+        dms = D.dedispersion_plan(nchan, DC.SMALL_DM_RANGE[0], DC.SMALL_DM_RANGE[1], f0, bw, ts)
+    D.dedisperse = _vec_dedisperse if patched else _orig_dedisperse
+    try:
+        with np.errstate(all="ignore"):
+            out = D._dedispersion_search(x, dms, nchan, f0, bw, ts)
+    finally:
+        D.dedisperse = _orig_dedisperse
+    return x, dms, out
+
+
+for case in DC.CASES:
+    k = DC.key(case)
+    if have(k + "_snr"):
+        continue
+    t0 = time.time()
+    small = case.startswith("small:")
+    x, dms, out = _deg_run(case, patched=not small)
+    if small:
+        # the vectorised dedisperse used for the large shapes gives the same bits here
+        with np.errstate(all="ignore"):
+            sh0 = D.dedispersion_shifts(x.shape[0], dms[-1], *DC.band(case)[1:])
+            a, b = _orig_dedisperse(x, sh0), _vec_dedisperse(x, sh0)
+        assert a.tobytes() == b.tobytes(), case
+        _, _, out2 = _deg_run(case, patched=True)
+        for u, v in zip(out, out2):
+            assert np.asarray(u).tobytes() == np.asarray(v).tobytes(), case
+    meta[k + "_input_sha256"] = sha(x)
+    arrays[k + "_dms"] = np.asarray(dms)
+    for col, v in zip(("max", "std", "snr", "rebin"), out):
+        arrays[f"{k}_{col}"] = np.asarray(v)
+    log("degenerate", case, x.shape, f"{time.time() - t0:.1f}s", "rebin", np.asarray(out[3])[:8],
+        "snr", np.asarray(out[2])[:4])
+
 np.savez_compressed(OUT_NPZ, **arrays)
 json.dump(meta, open(OUT_JSON, "w"), indent=1, sort_keys=True)
 log("wrote", OUT_NPZ, os.path.getsize(OUT_NPZ), "bytes;", len(arrays), "arrays,", len(meta), "meta")

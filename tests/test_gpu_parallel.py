@@ -48,7 +48,7 @@ def test_pipelined_tiles_equal_full_search(gpu, name, chunks):
     plan.search_tiles(xd, 0, 0, ws)
     plan.search_tiles(xd, ntt // 3, ntt, ws)
     plan.search_tiles(xd, 0, ntt // 3, ws)
-    for a, b in zip(full, plan.finalize(ws)):
+    for a, b in zip(full, plan.finalize(ws, xd)):
         np.testing.assert_array_equal(a, b.cpu().numpy())
     with pytest.raises(ValueError):
         plan.search_tiles(xd, 0, ntt + 1, ws)

@@ -146,3 +146,28 @@ def test_oracle_rebin_roll(golden):
         np.testing.assert_array_equal(co.quick_resample(x, r), arrays[f"resample_{r}"])
         np.testing.assert_array_equal(co.quick_chan_rebin(x, r), arrays[f"chanrebin_{r}"])
     np.testing.assert_array_equal(co.apply_dm_shifts(x, arrays["roll_shifts"]), arrays["roll_out"])
+
+
+# ------------------------------------------------------------------ degenerate trials
+import degenerate_cases as DC  # noqa: E402
+
+
+def _deg_inputs(golden, case):
+    arrays, meta = golden
+    k = DC.key(case)
+    x = DC.make(case)
+    assert sha(x) == meta[k + "_input_sha256"], case
+    return x, arrays[k + "_dms"], [arrays[f"{k}_{c}"] for c in ("max", "std", "snr", "rebin")]
+
+
+@pytest.mark.parametrize("case", [c for c in DC.CASES if not c.startswith("c2:")] + ["c2:block8:f32"])
+def test_oracle_degenerate_trials_bitexact(golden, case):
+    """The oracle's search reproduces the reference's degenerate-trial semantics bit for
+    bit (NaN-propagating max/std, NaN S/N never wins, +-inf S/N from a zero std, exact
+    and rounding-broken ties keep the first strictly larger S/N): golden tables from
+    executing the reference (make_golden.py, degenerate section)."""
+    x, dms, ref = _deg_inputs(golden, case)
+    _, f0, bw, ts = DC.band(case)
+    got = oracle.search(x, dms, f0, bw, ts, nthreads=8)
+    for g, r in zip(got, ref):
+        np.testing.assert_array_equal(g, r)
