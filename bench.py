@@ -75,7 +75,10 @@ def cpu_threads():
     return max(1, min(avail, int(env))) if env else avail
 
 
-def cpu_baseline(x_host, dms, cfg, ntrials, threads):
+def cpu_baseline(x_host, dms, cfg, ntrials, threads, reps=3):
+    """The C oracle (a port of the reference's numba prange search: float64, OpenMP over
+    trials) on ``ntrials`` evenly spaced trials of the same filterbank, ``reps`` times;
+    the median run is the value, the spread is reported beside it."""
     # OpenMP placement must be in the environment before libgomp initialises
     os.environ.setdefault("OMP_PROC_BIND", "close")
     os.environ.setdefault("OMP_PLACES", "cores")
@@ -83,26 +86,41 @@ def cpu_baseline(x_host, dms, cfg, ntrials, threads):
     ntrials = min(ntrials, dms.size)
     sel = dms[np.linspace(0, dms.size - 1, ntrials).astype(int)]
     oracle.search(x_host[:, :4096], sel[:2], cfg.start_freq, cfg.bandwidth, cfg.tsamp, nthreads=threads)
-    t0 = time.perf_counter()
-    oracle.search(x_host, sel, cfg.start_freq, cfg.bandwidth, cfg.tsamp, nthreads=threads)
-    dt = time.perf_counter() - t0
-    return {"value": ntrials * cfg.nsamples / dt, "unit": "DM-trial samples/s", "cores": threads,
+    runs = []
+    for _ in range(max(1, reps)):
+        t0 = time.perf_counter()
+        oracle.search(x_host, sel, cfg.start_freq, cfg.bandwidth, cfg.tsamp, nthreads=threads)
+        runs.append(ntrials * cfg.nsamples / (time.perf_counter() - t0))
+    med = float(np.median(runs))
+    return {"value": med, "unit": "DM-trial samples/s", "cores": threads,
             "kind": "port", "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+            "runs": [round(r, 1) for r in runs], "spread": round((max(runs) - min(runs)) / med, 4),
             "omp": {"OMP_PROC_BIND": os.environ.get("OMP_PROC_BIND"), "OMP_PLACES": os.environ.get("OMP_PLACES")},
             "sample": f"{ntrials} of the {dms.size} {cfg.name} trials (evenly spaced), full "
                       f"{cfg.nchan}x2^{int(np.log2(cfg.nsamples))} {cfg.dtype} filterbank, float64 "
-                      f"oracle/dedisp_oracle.c (numba prange -> OpenMP over trials), {dt:.1f} s"}
+                      f"oracle/dedisp_oracle.c (numba prange -> OpenMP over trials), median of {len(runs)} runs "
+                      f"of {ntrials * cfg.nsamples / med:.1f} s"}
 
 
-def load_pmc(workload):
-    """Per-launch HBM bytes of the dominant kernel from the committed PMC summary."""
-    path = os.path.join(REPO, "profiles", f"pmc_{workload}.json")
+def load_pmc(tag):
+    """Per-launch HBM bytes of the dominant kernel from the committed PMC summary
+    ``profiles/pmc_<tag>.json``, and whether it was collected from the kernel source this
+    library was built from (the summary records the SHA-256 of csrc/dedisperse.hip)."""
+    path = os.path.join(REPO, "profiles", f"pmc_{tag}.json")
     if not os.path.exists(path):
-        return None
+        return None, False
     try:
-        return json.load(open(path))
+        pmc = json.load(open(path))
     except (OSError, ValueError):
-        return None
+        return None, False
+    same = pmc.get("dedisperse_hip_sha256") == _hip.source_hashes().get("csrc/dedisperse.hip")
+    return pmc, same
+
+
+def knob_env():
+    """Every PU_* / PULSARUTILS_* variable: tuning knobs that reshape the kernels or the
+    library loaded (a bench line is only valid with none set)."""
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith(("PU_", "PULSARUTILS_"))}
 
 
 def clean_bench(dev, steps):
@@ -160,6 +178,76 @@ def clean_bench(dev, steps):
     return res
 
 
+def c3_strong(dev, world, rank, steps, chunks):
+    """configs[2] as BASELINE states it: the C3 filterbank (4096 chan x 2^22 uint8, 17.2 GB)
+    with its 5000 DM trials split contiguously over the N ranks (strong scaling).
+    ``compute_ms``: one search of every rank's slice on resident data (barrier + sync on
+    both sides, max over ranks); with N > 1 also the plain RCCL broadcast of the
+    filterbank and the chunked broadcast pipelined with the search (``end_to_end_ms``)."""
+    from pulsarutils.parallel import pipelined_broadcast_search
+    cfg = CONFIGS["C3"]
+    dms_all = dedispersion_plan(cfg.nchan, cfg.dmmin, cfg.dmmax, cfg.start_freq, cfg.bandwidth, cfg.tsamp)
+    lo, hi = shard_bounds(dms_all.size, world, rank)
+    dms = dms_all[lo:hi]
+    if rank == 0:
+        x = synth.pulsar_filterbank_device(cfg, device=dev)
+    else:
+        x = torch.empty((cfg.nchan, cfg.nsamples), dtype=torch.uint8, device=dev)
+    sh = _hip.shift_table(cfg.nchan, dms, cfg.start_freq, cfg.bandwidth, cfg.tsamp)
+    plan = _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, cfg.nchan, cfg.nsamples, sh)
+    ws = torch.empty(plan.workspace_bytes, dtype=torch.uint8, device=dev)
+    outs = plan._outs_ws(dev, None, ws)[0]
+    torch.cuda.synchronize()
+
+    def timed(fn):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        ms = torch.tensor([(time.perf_counter() - t0) * 1e3], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+        return float(ms.item())
+
+    res = {"workload": f"C3: {cfg.nchan} chan x 2^22 u8 samples, {dms_all.size} DM trials split over {world} GPU(s)",
+           "scaling": "strong", "trials_per_gpu": int(hi - lo), "group": plan.info["group"], "steps": steps}
+    if world > 1:
+        res["broadcast_ms"] = timed(lambda: dist.broadcast(x, src=0))
+        res["end_to_end_ms"] = timed(lambda: pipelined_broadcast_search(x, plan, outs, ws, src=0, chunks=chunks))
+        res["end_to_end_samples_per_s"] = dms_all.size * cfg.nsamples / (res["end_to_end_ms"] / 1e3)
+        res["bcast_chunks"] = chunks
+    plan.search(x, out=outs, workspace=ws)  # warm-up
+    plan.enable_timing(steps)
+
+    def search_steps():
+        for _ in range(steps):
+            plan.search(x, out=outs, workspace=ws)
+
+    res["compute_ms"] = timed(search_steps) / steps
+    kms = plan.kernel_times_ms(steps)
+    res["kernel_ms_rank0"] = float(np.mean(kms)) if len(kms) else None
+    res["value"] = dms_all.size * cfg.nsamples / (res["compute_ms"] / 1e3)
+    res["unit"] = "DM-trial samples/s"
+    snr = outs[2].clone()
+    if world > 1:
+        chunk = -(-dms_all.size // world)
+        loc = torch.full((chunk,), -1.0, dtype=torch.float64, device=dev)
+        loc[:hi - lo] = snr
+        allv = torch.empty((world, chunk), dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(allv, loc)
+        snr = torch.cat([allv[r, :shard_bounds(dms_all.size, world, r)[1] - shard_bounds(dms_all.size, world, r)[0]]
+                         for r in range(world)])
+    res["best_dm"] = float(dms_all[int(torch.argmax(snr).item())])
+    res["certify"] = plan.cert_info()
+    del x, ws, outs, plan
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -168,12 +256,26 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--acc", default="native", choices=["native", "f32", "f64"])
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--shard", type=int, default=0,
+                    help="with --scaling strong on one GPU: search only rank 0's slice of an N-way split "
+                         "(e.g. --config C3 --scaling strong --shard 8: the 625-trial shard of the 8-GPU run)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-trials", type=int, default=400)
     ap.add_argument("--no-clean", action="store_true")
     ap.add_argument("--clean-steps", type=int, default=5)
     ap.add_argument("--bcast-chunks", type=int, default=8)
+    ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--no-c3-strong", action="store_true",
+                    help="skip the configs[2] sub-benchmark (C3: 5000 trials split over the N GPUs)")
+    ap.add_argument("--c3-steps", type=int, default=2)
+    ap.add_argument("--allow-knobs", action="store_true",
+                    help="time even with PU_* / PULSARUTILS_* tuning variables set (sweeps only: the line "
+                         "is marked invalid)")
     args = ap.parse_args()
+    knobs = knob_env()
+    if knobs and not args.allow_knobs:
+        sys.exit(f"bench.py: refusing to time with tuning variables set {knobs} (they reshape the kernels or "
+                 "swap the library; unset them, or pass --allow-knobs for a sweep)")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -198,6 +300,9 @@ def main():
     else:
         dms_all = dedispersion_plan(cfg.nchan, cfg.dmmin, cfg.dmmax, cfg.start_freq, cfg.bandwidth, cfg.tsamp)
     lo, hi = shard_bounds(dms_all.size, world, rank)
+    if args.shard > 1 and world == 1 and args.scaling == "strong":
+        lo, hi = shard_bounds(dms_all.size, args.shard, 0)
+        dms_all = dms_all[lo:hi]
     dms = dms_all[lo:hi]
     per_rank = dms.size
     chunk = -(-dms_all.size // world)  # equal gather slots
@@ -268,6 +373,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kms = plan.kernel_times_ms(args.steps)
+    cert = plan.cert_info()
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -295,21 +401,28 @@ def main():
         acc64 = bool(info["acc_is_f64"])
         peak = VALU_F64_ADD_PEAK_TFLOPS if acc64 else VALU_ADD_PEAK_TFLOPS
         achieved = adds / (kernel_ms / 1e3) / 1e12
-        pmc = load_pmc(args.config) if world == 1 or args.scaling == "weak" else None
-        traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+        pmc_tag = args.config if per_rank == cfg.ntrials else f"{args.config}_{per_rank}"
+        pmc, pmc_same = load_pmc(pmc_tag)
+        # counter traffic only when it was collected from this kernel source
+        traffic = pmc.get("hbm_bytes_per_launch") if pmc and pmc_same else None
         roof = {"bound": "valu", "achieved": round(achieved, 3), "peak": peak,
                 "unit": "TFLOP/s" + (" (f64 adds)" if acc64 else " (f32 adds)"),
                 "frac": round(achieved / peak, 4), "traffic": traffic,
                 "kernel": "dedisp_sub_kernel" if info["group"] > 1 else "dedisp_kernel",
                 "kernel_ms": round(kernel_ms, 4),
                 "algorithmic_flop_per_launch": adds, "algorithmic_bytes_per_launch": alg_bytes,
+                "time_tiles": info["time_tiles"],
                 "hbm_compulsory_gbs": round(alg_bytes / (kernel_ms / 1e3) / 1e9, 1),
                 "hbm_compulsory_frac": round(alg_bytes / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
         if traffic:
             roof.update({"hbm_counter_GBps": round(traffic / (kernel_ms / 1e3) / 1e9, 1),
                          "hbm_counter_frac": round(traffic / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "traffic_source": pmc.get("source"), "traffic_kernel_ms_at_collection":
-                             pmc.get("kernel_ms_at_collection")})
+                         "traffic_source": f"profiles/pmc_{pmc_tag}.json ({pmc.get('source')})",
+                         "traffic_kernel_ms_at_collection": pmc.get("kernel_ms_at_collection"),
+                         "traffic_source_sha256_matches_build": True})
+        elif pmc:
+            roof["traffic_note"] = (f"profiles/pmc_{pmc_tag}.json was collected from another dedisperse.hip "
+                                    "(SHA-256 differs): not reported")
         if info["group"] > 1:
             # executed work of the exact subband decomposition: G x fewer
             # adds than the algorithm's; the LDS array (256 B/clk/CU) is its binding unit
@@ -331,9 +444,18 @@ def main():
         log("cpu baseline ...")
         xh = x.cpu().numpy()
         threads = cpu_threads()
-        cpu = cpu_baseline(xh, dms, cfg, args.cpu_trials, threads)
+        cpu = cpu_baseline(xh, dms, cfg, args.cpu_trials, threads, reps=args.cpu_reps)
         del xh
         log(f"cpu baseline {cpu['value']:.3e} samples/s on {threads} threads ({cpu['cpu_model']})")
+
+    c3 = None
+    if not args.no_c3_strong and args.config != "C3":
+        del x, ws, outs, plan
+        torch.cuda.empty_cache()
+        log("c3_strong ...")
+        c3 = c3_strong(dev, world, rank, args.c3_steps, args.bcast_chunks)
+        if rank == 0:
+            log(f"c3_strong compute {c3['compute_ms']:.1f} ms, end-to-end {c3.get('end_to_end_ms')}")
 
     if rank == 0:
         line = {"metric": "dedispersed DM-trial samples/sec (whole node)", "value": value,
@@ -349,7 +471,12 @@ def main():
                            "nchan": cfg.nchan, "nsamples": cfg.nsamples, "trials_per_gpu": per_rank,
                            "total_trials": int(dms_all.size), "parallelism": f"dm-shard{world}",
                            "best_dm": best_dm},
-                "roofline": roof, "clean": clean, "cpu_baseline": cpu}
+                "roofline": roof, "clean": clean, "cpu_baseline": cpu,
+                "certify": dict(cert, what="trials of the last timed step whose fast statistics could not be "
+                                           "certified and were recomputed exactly (DESIGN.md §4.5)"),
+                "env": knobs, "valid": not knobs}
+        if c3 is not None:
+            line["c3_strong"] = c3
         if bcast is not None:
             line["multi_gpu"] = bcast
         line["build"] = _hip.build_info()  # was the library built from the sources shipped with it

@@ -13,7 +13,9 @@
  *    are marked "host".  Row-major 2-D arrays carry a leading dimension ``ld``
  *    (elements).
  *  - Calls are asynchronous on ``stream`` (a hipStream_t passed as void*; NULL = the
- *    null stream) and never throw.  They return PU_OK (0) or a negative PU_E* code;
+ *    null stream) and never throw - except pu_plan_search / pu_plan_finalize, which
+ *    synchronise ``stream`` once to settle their certification step (see
+ *    pu_plan_finalize) and return final outputs.  They return PU_OK (0) or a negative PU_E* code;
  *    pu_last_error() returns a thread-local message for the last failure.
  *  - The caller selects the device (hipSetDevice) before calling.
  */
@@ -149,11 +151,25 @@ int pu_plan_stamps(pu_plan *plan, int64_t *out, int n);
 /* Introspection (tests / DESIGN.md): fills up to ``n`` of
  * {ndm, dm_tiles, time_tiles, trials_per_tile, time_tile, chans_per_step,
  *  row_stride, lds_bytes, acc_is_f64, max_spread, group, slots, stages,
- *  slot_bytes, raw_stride, exec_adds, lds_traffic, cert_rechecked, cert_nan}: exec_adds
- *  and lds_traffic are the adds and LDS bytes (reads, writes, DMA) one launch executes
- *  (subband mode; 0 otherwise); the last two describe the last search's certification
- *  step (see pu_plan_finalize).  Returns the count written. */
+ *  slot_bytes, raw_stride, exec_adds, lds_traffic, cert_rechecked, cert_nan, cert_std,
+ *  cert_sign, cert_tie, cert_us}: exec_adds and lds_traffic are the adds and LDS bytes (reads,
+ *  writes, DMA) one launch executes (subband mode; 0 otherwise); the cert_* fields
+ *  describe the last search's certification step (see pu_plan_finalize): trials
+ *  recomputed, the NaN rule, and how many trials each check flagged (std not above its
+ *  rounding bound, S/N sign, S/N tie) and the host microseconds spent settling them.
+ *  Returns the count written. */
 int pu_plan_info(const pu_plan *plan, int64_t *info, int n);
+
+/* ------------------------------------------------------------------ streams */
+
+/* A compute stream on the current device whose CU mask leaves ``reserve`` CUs out
+ * (spread over the XCDs), for launching the search while an RCCL collective runs on
+ * another stream: the collective's workgroups find those CUs free (the search holds one
+ * 160 KiB-LDS workgroup per CU).  No reference counterpart (multi-GPU path, DESIGN.md
+ * §5; the reference's parallelism is numba prange, dedispersion.py:181).
+ * *stream: hipStream_t as void*, released with pu_stream_destroy. */
+int pu_stream_create_cu_masked(int reserve, void **stream);
+int pu_stream_destroy(void *stream);
 
 /* ------------------------------------------------------------------ cleaning */
 

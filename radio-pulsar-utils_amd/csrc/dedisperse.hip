@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
 #include <cmath>
 #include <cstdlib>
@@ -325,10 +326,23 @@ __device__ __forceinline__ void stats_full_pairs(const f32x2 (&acc)[D][J], const
                                                  int cnt, int tt, int lane)
 {
     const bool even = (lane & 1) == 0, quad = (lane & 3) == 0;
+    // The shift (recorded as the partial's center): the tile mean of the wave's first
+    // trial.  The wave's D trials are a few DM steps apart, so their tile means differ by
+    // a small fraction of the std: the shifted squares stay near the variance and their
+    // float32 sums stay accurate, which keeps the finalize's certification bound tight
+    // (lane 0's first sample as the shift inflated them by w^2 var).
+    float kt;
+    {
+        f32x2 s0 = acc[0][0];
+#pragma unroll
+        for (int j = 1; j < J; ++j) s0 += acc[0][j];
+        const float v = wave_sum_to63(s0.x + s0.y);
+        kt = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63)) *
+             (1.0f / (128.0f * J));
+    }
 #pragma unroll
     for (int d = 0; d < D; ++d) {
         if (slot0 + d >= cnt) continue;
-        const float kt = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, acc[d][0].x), 0));
         const f32x2 k1 = {kt, kt};
         const float k2 = 2.0f * kt, k4 = 4.0f * kt, k8 = 8.0f * kt;
         f32x2 s1 = {0.0f, 0.0f}, q1 = s1;
@@ -693,7 +707,7 @@ struct SubArgs {
     int32_t raw_stride;     // elements per staged channel row (DMA mode; bytes for 8-bit rows)
     int32_t zero_len;       // floats of the zero row at LDS offset 0 (DMA mode, partial groups)
     int32_t lds_bytes;      // dynamic LDS size: a stage's raw rows end here
-    int32_t skip;           // tuning ablation (PU_SUB_SKIP; results invalid): 1 build, 2 sum, 4 DMA
+    int32_t skip;           // diagnostic build only (PU_SUB_SKIP; results invalid): 1 build, 2 sum, 4 DMA, 8 epilogue
     int32_t dma_waves;      // waves that issue the LDS-DMA rows (the last ones of the workgroup)
     int32_t nitems;         // work items (DM tiles x time tiles of this launch)
     int32_t base_bits;      // DMA row words: base = word & (2^base_bits - 1), cover = (word >> base_bits) x 256 B
@@ -918,6 +932,11 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
     // instructions behind everyone's on the CU's one texture-address path.
     const int32_t *base_t = base_tab + (size_t)dt * o.nchan;
     const int NDW = a.dma_waves;
+#ifdef PU_STAMPS
+    int skip = a.skip;  // diagnostic build only: PU_SUB_SKIP ablation (results invalid)
+#else
+    constexpr int skip = 0;  // the production kernel always does all of its work
+#endif
     const int dw = wave - (W - NDW);  // < 0: this wave issues no DMA
     auto bases_of = [&](const i32x4 st) -> int {
         const int c = st.x * G + dw + NDW * lane;
@@ -1091,7 +1110,7 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
         __syncthreads();  // raw rows of stage k landed; every wave left the slot area
         PU_PHASE(1);
         const int vb1 = kDma && k + 1 < ns ? bases_of(st1) : 0;  // lands during the build
-        if (!(a.skip & 1)) build(st, m0);
+        if (!(skip & 1)) build(st, m0);
         PU_PHASE(2);
         __syncthreads();  // slots built; every wave left the raw rows
         PU_PHASE(3);
@@ -1105,7 +1124,7 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
             // the DMAs just issued - every DMA wave then summed only after its rows landed.
             int vb = vb1;
             asm volatile("" : "+v"(vb));
-            if (k + 1 < ns && !(a.skip & 4)) issue_raw(st1, vb, 0, rows_of(st1));
+            if (k + 1 < ns && !(skip & 4)) issue_raw(st1, vb, 0, rows_of(st1));
         }
         PU_PHASE(4);
         // The DMA waves start summing last (their LDS-DMA issue holds them ~10 % of the
@@ -1113,7 +1132,7 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
         // around them instead of reaching the barrier first and leaving it half idle
         // (C2 17.3 -> 16.9 ms; raising it for the DMA issue too: 17.6).
         if (dw >= 0) __builtin_amdgcn_s_setprio(1);
-        if (active && !(a.skip & 2)) {
+        if (active && !(skip & 2)) {
             const uint32_t sb = smem_addr + 8u * lane;  // window records: absolute LDS offsets
             // two groups per iteration with ping-pong records (no per-group record copy).
             // A record is consumed only after the previous group's last lgkmcnt(0) (the empty
@@ -1138,12 +1157,12 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
         st1 = st2;
     }
     if constexpr (STATS && !PLANE) {
-        if (active && !(a.skip & 8) && t0 + TT <= n) {
+        if (active && !(skip & 8) && t0 + TT <= n) {
             stats_full_pairs<D, C::J>(acc2, o, first, slot0, cnt, tt, lane);
 #ifndef PU_STAMPS
             return;
 #else
-            a.skip |= 8;  // stamps build: the epilogue is done, only the stamps remain
+            skip |= 8;  // stamps build: the epilogue is done, only the stamps remain
 #endif
         }
     }
@@ -1156,7 +1175,7 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
             acc[d][2 * m + 1] = acc2[d][m].y;
         }
 #ifdef PU_STAMPS
-    if (active && !(a.skip & 8)) write_outputs<float, float, K, D, PLANE, STATS>(acc, o, first, slot0, cnt, t0, tt, lane);
+    if (active && !(skip & 8)) write_outputs<float, float, K, D, PLANE, STATS>(acc, o, first, slot0, cnt, t0, tt, lane);
     PU_PHASE(6);
     if (lane == 0 && a.stamps) {
         for (int i = 0; i < 8; ++i) atomicAdd(reinterpret_cast<unsigned long long *>(a.stamps) + i,
@@ -1165,7 +1184,7 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
 #undef PU_PHASE
 #else
 #undef PU_PHASE
-    if (!active || (a.skip & 8)) return;
+    if (!active || (skip & 8)) return;
     write_outputs<float, float, K, D, PLANE, STATS>(acc, o, first, slot0, cnt, t0, tt, lane);
 #endif
 }
@@ -1190,7 +1209,8 @@ struct CertState {
     int32_t nflag;       // trials the fast path could not certify (listed after the state)
     int32_t nnonfinite;  // of which: a non-finite partial (NaN / inf in the series)
     int32_t scan;        // non-finite input scan (pu::nonfinite_any_async)
-    int32_t pad[61];
+    int32_t why[3];      // flagged by: std not above its bound, S/N sign, S/N tie
+    int32_t pad[58];
 };
 static_assert(sizeof(CertState) == 256, "CertState");
 
@@ -1239,7 +1259,10 @@ pu_finalize_kernel(const double *__restrict__ part, int ntt, int n, int tt_len,
             const double wd = width * dk;
             S1[w] += s1 + cntb * wd;
             S2[w] += s2 + 2.0 * wd * s1 + cntb * wd * wd;
-            A2[w] += fabs(s2) + cntb * wd * wd;
+            // magnitude the rounding bound scales with: the tile's sum of squares (relative
+            // error gamma), its recentring term through s1 (|d s1| <= gamma sum|y| <=
+            // gamma sqrt(cnt s2)), and 2^-30 of the float64 recentring square
+            A2[w] += fabs(s2) + 2.0 * fabs(wd) * sqrt(cntb * fabs(s2)) + 0x1p-30 * cntb * wd * wd;
             // NaN-propagating (a NaN partial max makes the trial non-finite below)
             MX[w] = (q[1 + 3 * w] > MX[w] || q[1 + 3 * w] != q[1 + 3 * w]) ? q[1 + 3 * w] : MX[w];
         }
@@ -1287,6 +1310,7 @@ pu_finalize_kernel(const double *__restrict__ part, int ntt, int n, int tt_len,
             }
         }
         bool uncertain = false;
+        int why = -1;
         if (!nonfinite) {
             const double E = cm.e_rel * (fabs(mean) + 4.0 * sdw[0] + fabs(red[2][0][0]));
             double b = 0.0, eb = 0.0;  // the reference's (best_snr, its bound) chain
@@ -1297,18 +1321,25 @@ pu_finalize_kernel(const double *__restrict__ part, int ntt, int n, int tt_len,
                 const double e_var = 4.0 * cm.gamma * Qw[w];
                 const double e_sd = sd > 0 ? e_var / sd + width * E : INFINITY;
                 const double num = MXw - width * mean;
-                const double e_num = 2.0 * width * E + cm.gamma * (fabs(MXw) + width * sqrt(Qw[0])) +
+                // max - w mean: the series error, the mean's rounding (through S1), the
+                // float64 combination, and - unless the rebinned sums are exact (exact-series
+                // plans: integers < 2^24 or float64) - their float32 rounding
+                const double e_num = 2.0 * width * E + cm.gamma * width * sqrt(Qw[0]) +
+                                     (cm.tie_check ? 0.0 : cm.gamma * fabs(MXw)) +
                                      0x1p-50 * (fabs(MXw) + width * fabs(mean));
                 if (!(e_sd <= 0.25 * sd) || !(fabs(num) > e_num)) {
                     uncertain = true;
+                    why = !(e_sd <= 0.25 * sd) ? 0 : 1;
                     break;
                 }
                 const double snr = num / sd;
                 const double e_snr = (e_num + fabs(snr) * e_sd) / (sd - e_sd) + 0x1p-44 * fabs(snr);
                 if (cm.tie_check) {
                     const double d = snr - b;
-                    if (!(fabs(d) > e_snr + eb)) uncertain = true;
-                    else if (d > 0) {
+                    if (!(fabs(d) > e_snr + eb)) {
+                        uncertain = true;
+                        why = 2;
+                    } else if (d > 0) {
                         b = snr;
                         eb = e_snr;
                     }
@@ -1318,6 +1349,7 @@ pu_finalize_kernel(const double *__restrict__ part, int ntt, int n, int tt_len,
         if (nonfinite || uncertain) {
             list[atomicAdd(&cert->nflag, 1)] = trial;
             if (nonfinite) atomicAdd(&cert->nnonfinite, 1);
+            if (why >= 0) atomicAdd(&cert->why[why], 1);
         }
         max_out[trial] = red[2][0][0] - mean;
         std_out[trial] = sdw[0];
@@ -1393,7 +1425,9 @@ struct pu_plan {
     // flagged trials, a pinned copy of the device CertState, the last call's outcome
     std::vector<int64_t> shifts;
     CertState *h_cert = nullptr;
-    int64_t cert_rechecked = 0, cert_nan = 0;
+    int64_t cert_rechecked = 0, cert_nan = 0, cert_why[3] = {0, 0, 0}, cert_us = 0;
+    void *rc_buf = nullptr;  // recheck scratch (series, pu_series_stats workspace, shifts, indices)
+    size_t rc_bytes = 0;
 };
 
 namespace {
@@ -1450,10 +1484,13 @@ int launch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
     sa.raw_stride = p->raw_stride;
     sa.zero_len = (int32_t)p->zero_len;
     sa.lds_bytes = (int32_t)p->lds_bytes;
-    if (const char *env = getenv("PU_SUB_SKIP")) sa.skip = atoi(env);
     sa.stamps = p->d_stamps;
     sa.dma_waves = std::min<int>(8, C::W);  // C2 17.6 vs 18.95 ms with all 16 waves, C3 141 vs 150 (625 trials)
+#ifdef PU_STAMPS
+    // diagnostic build only (make stamps): ablation and DMA-wave tuning knobs
+    if (const char *env = getenv("PU_SUB_SKIP")) sa.skip = atoi(env);
     if (const char *env = getenv("PU_DMA_WAVES")) sa.dma_waves = std::clamp(atoi(env), 1, (int)C::W);
+#endif
 
     const int64_t nitems = (int64_t)p->ndt * a.ntt_run;
     sa.nitems = (int32_t)nitems;
@@ -1541,6 +1578,7 @@ void free_plan(pu_plan *p)
     (void)hipFree(p->d_recs);
     (void)hipFree(p->d_stamps);
     if (p->h_cert) (void)hipHostFree(p->h_cert);
+    (void)hipFree(p->rc_buf);
     delete p;
 }
 
@@ -2048,9 +2086,13 @@ CertModel cert_model(const pu_plan *p)
         m.e_rel = 0x1p-50;
         m.gamma = 0x1p-44;
     } else if (p->dtype == PU_U8 && 8 * 255 * p->nchan < (int64_t(1) << 24)) {
-        m.tie_check = 1;  // integer sums (and their 8-sample rebins) below 2^24: exact in float32
+        // integer sums (and their 8-sample rebins) below 2^24: exact in float32.  The
+        // epilogue's sums of squares: <= 12 float32 roundings of nonnegative terms (the
+        // square, 4 lane-local adds, the pair add, 4 row-reduction adds, the shifted
+        // value itself twice) = 12 x 2^-24 < 2^-20
+        m.tie_check = 1;
         m.e_rel = 0.0;
-        m.gamma = 0x1p-19;
+        m.gamma = 0x1p-20;
     } else {
         // float32 sums of float data: the typical (random-walk) rounding of nchan terms
         // with an 8x margin, relative to the series' magnitude; S/N ties within the
@@ -2076,9 +2118,10 @@ int launch_finalize(pu_plan *p, const double *part, double *mx, double *sd, doub
 // After the finalize kernel: wait for it, then settle the flagged trials.  An input
 // holding NaN / inf (found by a scan, run only when some trial saw a non-finite value)
 // gives every trial the reference's NaN result; other flagged trials are recomputed
-// exactly - float64 channel-order dedispersion (a channel-mode sub-plan of the flagged
-// trials' shifts: the reference's series bit for bit) + pu_series_stats - in batches
-// that fit ~1 GiB of scratch.
+// exactly - their float64 channel-order series (the reference's bit for bit, by a direct
+// gather: ~1 ms per trial at C3, far below a channel-mode sub-plan's cost for the
+// few trials a search flags) + pu_series_stats - in batches that fit ~1 GiB of scratch
+// kept with the plan.
 int resolve_flagged(pu_plan *p, const void *data, int64_t ld, double *mx, double *sd, double *snr, int32_t *win,
                     char *ws, hipStream_t s)
 {
@@ -2089,7 +2132,19 @@ int resolve_flagged(pu_plan *p, const void *data, int64_t ld, double *mx, double
     PU_TRY_HIP(hipMemcpyAsync(p->h_cert, cert, sizeof(CertState), hipMemcpyDeviceToHost, s));
     PU_TRY_HIP(hipStreamSynchronize(s));
     const int64_t nflag = p->h_cert->nflag;
+    for (int k = 0; k < 3; ++k) p->cert_why[k] = p->h_cert->why[k];
+    p->cert_us = 0;
     if (nflag == 0) return PU_OK;
+    const auto t_start = std::chrono::steady_clock::now();
+    struct Timer {  // host time spent settling the flagged trials (pu_plan_info cert_us)
+        pu_plan *p;
+        std::chrono::steady_clock::time_point t0;
+        ~Timer()
+        {
+            p->cert_us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0)
+                             .count();
+        }
+    } timer{p, t_start};
     if (p->h_cert->nnonfinite > 0 && p->dtype != PU_U8) {
         int rc = pu::nonfinite_any_async(data, p->dtype, p->nchan, p->n, ld, &cert->scan, s);
         if (rc) return rc;
@@ -2111,35 +2166,42 @@ int resolve_flagged(pu_plan *p, const void *data, int64_t ld, double *mx, double
     PU_TRY_HIP(hipStreamSynchronize(s));
     std::sort(idx.begin(), idx.end());
     const int64_t n = p->n, nchan = p->nchan;
-    const int64_t per_row = n * 8 + (int64_t)pu_series_stats_workspace_bytes(1, n);
+    const int64_t per_row = n * 8 + (int64_t)pu_series_stats_workspace_bytes(1, n) + nchan * 8;
     const int64_t B = std::max<int64_t>(1, std::min<int64_t>(nflag, (int64_t(1) << 30) / per_row));
-    double *plane = nullptr;
-    void *sws = nullptr;
-    int32_t *d_idx = nullptr;
-    const size_t sws_bytes = pu_series_stats_workspace_bytes(B, n);
-    int rc = pu::hip_check(hipMalloc((void **)&plane, (size_t)B * n * sizeof(double)), "hipMalloc(recheck plane)");
-    if (!rc) rc = pu::hip_check(hipMalloc(&sws, sws_bytes), "hipMalloc(recheck workspace)");
-    if (!rc) rc = pu::hip_check(hipMalloc((void **)&d_idx, (size_t)B * sizeof(int32_t)), "hipMalloc(recheck index)");
+    const size_t plane_b = ((size_t)B * n * sizeof(double) + 255) & ~size_t(255);
+    const size_t sws_b = (pu_series_stats_workspace_bytes(B, n) + 255) & ~size_t(255);
+    const size_t sh_b = ((size_t)B * nchan * sizeof(int64_t) + 255) & ~size_t(255);
+    const size_t need = plane_b + sws_b + sh_b + (size_t)B * sizeof(int32_t);
+    if (p->rc_bytes < need) {  // scratch kept with the plan, grown on demand
+        (void)hipFree(p->rc_buf);
+        p->rc_buf = nullptr;
+        p->rc_bytes = 0;
+        PU_TRY_HIP(hipMalloc(&p->rc_buf, need));
+        p->rc_bytes = need;
+    }
+    char *sc = reinterpret_cast<char *>(p->rc_buf);
+    double *plane = reinterpret_cast<double *>(sc);
+    void *sws = sc + plane_b;
+    int64_t *d_sh = reinterpret_cast<int64_t *>(sc + plane_b + sws_b);
+    int32_t *d_idx = reinterpret_cast<int32_t *>(sc + plane_b + sws_b + sh_b);
     std::vector<int64_t> sh;
+    int rc = PU_OK;
     for (int64_t i0 = 0; !rc && i0 < nflag; i0 += B) {
         const int64_t m = std::min(B, nflag - i0);
         sh.resize((size_t)(m * nchan));
         for (int64_t k = 0; k < m; ++k)
             std::copy_n(p->shifts.data() + (size_t)idx[(size_t)(i0 + k)] * nchan, nchan, sh.data() + k * nchan);
-        pu_plan *q = nullptr;
-        rc = pu_plan_create_grouped(&q, p->dtype, PU_ACC_F64, nchan, n, sh.data(), m, 1);
-        if (!rc) rc = pu_plan_dedisperse(q, data, ld, plane, n, s);
+        for (auto &v : sh) v = ((v % n) + n) % n;  // row index (t + shift) mod n
+        rc = pu::hip_check(hipMemcpyAsync(d_sh, sh.data(), sh.size() * sizeof(int64_t), hipMemcpyHostToDevice, s),
+                           "hipMemcpyAsync(recheck shifts)");
+        if (!rc) rc = pu::exact_series(data, p->dtype, nchan, n, ld, d_sh, m, plane, s);
         if (!rc)
             rc = pu::hip_check(hipMemcpyAsync(d_idx, idx.data() + i0, (size_t)m * sizeof(int32_t),
                                               hipMemcpyHostToDevice, s), "hipMemcpyAsync(recheck index)");
-        if (!rc) rc = pu_series_stats(plane, m, n, n, d_idx, mx, sd, snr, win, sws, sws_bytes, s);
+        if (!rc) rc = pu_series_stats(plane, m, n, n, d_idx, mx, sd, snr, win, sws, sws_b, s);
         const int rs = pu::hip_check(hipStreamSynchronize(s), "hipStreamSynchronize(recheck)");
         if (!rc) rc = rs;
-        if (q) pu_plan_destroy(q);
     }
-    (void)hipFree(plane);
-    (void)hipFree(sws);
-    (void)hipFree(d_idx);
     if (!rc) p->cert_rechecked = nflag;
     return rc;
 }
@@ -2332,7 +2394,8 @@ int pu_plan_info(const pu_plan *p, int64_t *info, int n)
     const int64_t v[] = {p->ndm, p->ndt, p->ntt, p->group > 1 ? with_shape(p->shape, [](auto c) { return decltype(c)::T; }) : kTPT, p->TT, p->ncc,
                          p->row_stride, (int64_t)p->lds_bytes, kVariants[p->variant].acc_f64, p->max_spread,
                          p->group, p->nslots_total, p->nstages, (int64_t)p->slot_bytes, p->raw_stride,
-                         p->exec_adds, p->lds_traffic, p->cert_rechecked, p->cert_nan};
+                         p->exec_adds, p->lds_traffic, p->cert_rechecked, p->cert_nan, p->cert_why[0],
+                         p->cert_why[1], p->cert_why[2], p->cert_us};
     const int m = std::min<int>(n, (int)(sizeof v / sizeof v[0]));
     for (int k = 0; k < m; ++k) info[k] = v[k];
     return m;

@@ -11,6 +11,12 @@ namespace pu {
 int nonfinite_any_async(const void *data, int dtype, int64_t nrows, int64_t n, int64_t ld, int32_t *flag,
                         hipStream_t s);
 
+// The reference's dedispersed series (float64, channel order: bit-identical) of ``rows``
+// trials whose shifts (device, rows x nchan, each reduced to [0, n)) are given, into
+// out (rows x n).  A direct gather: for a handful of trials (certification rechecks).
+int exact_series(const void *data, int dtype, int64_t nchan, int64_t n, int64_t ld, const int64_t *shifts, int64_t rows,
+                 double *out, hipStream_t s);
+
 // The reference's result for every trial when the input holds a non-finite value:
 // max = std = NaN, snr = 0, rebin = 0 (dedispersion.py:186-201).
 int nan_rule(int64_t ndm, double *max_out, double *std_out, double *snr_out, int32_t *win_out, hipStream_t s);

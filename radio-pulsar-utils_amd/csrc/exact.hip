@@ -112,6 +112,42 @@ __global__ void exact_final_kernel(int64_t rows, int64_t n, const uint64_t *__re
     win_out[o] = bestw;
 }
 
+// The reference's dedispersed series of a few trials, directly: out[r][t] =
+// ((0 + x[0][(t + s[r][0]) mod n]) + x[1][...]) + ... in float64, channel order
+// (roll_and_sum's order, dedispersion.py:60-98: bit-identical).  Each thread owns 4
+// consecutive samples; a wave reads 256 consecutive elements of a row per channel.  The
+// row shifts (in [0, n)) go through LDS 1024 channels at a time.
+template <typename T>
+__global__ void __launch_bounds__(256)
+exact_series_kernel(const T *__restrict__ x, int64_t ld, int64_t nchan, int64_t n, const int64_t *__restrict__ shifts,
+                    double *__restrict__ out)
+{
+    __shared__ int64_t sh[1024];
+    const int64_t r = blockIdx.y;
+    const int64_t t0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int64_t c0 = 0; c0 < nchan; c0 += 1024) {
+        const int64_t nc = nchan - c0 < 1024 ? nchan - c0 : 1024;
+        __syncthreads();
+        for (int64_t i = threadIdx.x; i < nc; i += 256) sh[i] = shifts[r * nchan + c0 + i];
+        __syncthreads();
+        if (t0 >= n) continue;
+        for (int64_t ci = 0; ci < nc; ++ci) {
+            const T *row = x + (c0 + ci) * ld;
+            int64_t idx = t0 + sh[ci];
+            if (idx >= n) idx -= n;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (t0 + k < n) acc[k] += static_cast<double>(row[idx]);
+                if (++idx == n) idx = 0;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (t0 + k < n) out[r * n + t0 + k] = acc[k];
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256)
 nonfinite_scan_kernel(const T *__restrict__ x, int64_t nrows, int64_t n, int64_t ld, int32_t *flag)
@@ -230,6 +266,28 @@ int nonfinite_any_async(const void *data, int dtype, int64_t nrows, int64_t n, i
     else
         return PU_OK;  // integers are always finite (the flag stays 0)
     return launch_check("nonfinite_scan_kernel");
+}
+
+int exact_series(const void *data, int dtype, int64_t nchan, int64_t n, int64_t ld, const int64_t *shifts, int64_t rows,
+                 double *out, hipStream_t s)
+{
+    const dim3 grid((unsigned)((n + 1023) / 1024), (unsigned)rows), blk(256);
+    switch (dtype) {
+    case PU_U8:
+        hipLaunchKernelGGL(exact_series_kernel<uint8_t>, grid, blk, 0, s, reinterpret_cast<const uint8_t *>(data), ld,
+                           nchan, n, shifts, out);
+        break;
+    case PU_F32:
+        hipLaunchKernelGGL(exact_series_kernel<float>, grid, blk, 0, s, reinterpret_cast<const float *>(data), ld,
+                           nchan, n, shifts, out);
+        break;
+    case PU_F64:
+        hipLaunchKernelGGL(exact_series_kernel<double>, grid, blk, 0, s, reinterpret_cast<const double *>(data), ld,
+                           nchan, n, shifts, out);
+        break;
+    default: set_error("exact_series: dtype %d", dtype); return PU_EUNSUPPORTED;
+    }
+    return launch_check("exact_series_kernel");
 }
 
 int nan_rule(int64_t ndm, double *max_out, double *std_out, double *snr_out, int32_t *win_out, hipStream_t s)

@@ -59,11 +59,14 @@ SIGNATURES = {
     "pu_roll_rows": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp]),
     "pu_roll_and_sum": (_i32, [_vp, _i32, _i64, _i64, _vp, _vp]),
     "pu_transpose": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _i64, _vp]),
+    "pu_stream_create_cu_masked": (_i32, [_i32, ctypes.POINTER(_vp)]),
+    "pu_stream_destroy": (_i32, [_vp]),
 }
 
 INFO_FIELDS = ("ndm", "dm_tiles", "time_tiles", "trials_per_tile", "time_tile", "chans_per_step",
                "row_stride", "lds_bytes", "acc_is_f64", "max_spread", "group", "slots", "stages",
-               "slot_bytes", "raw_stride", "exec_adds", "lds_traffic", "cert_rechecked", "cert_nan")
+               "slot_bytes", "raw_stride", "exec_adds", "lds_traffic", "cert_rechecked", "cert_nan", "cert_std", "cert_sign",
+               "cert_tie", "cert_us")
 
 
 class HipBackendError(RuntimeError):
@@ -250,7 +253,10 @@ class Plan:
         copy is made ON the launch stream (so it is ordered after whatever that stream
         waits for, and the caching allocator only reuses its memory after that stream's
         later work, i.e. after the kernel that reads it)."""
-        if data.element_size() == 1 and (data.data_ptr() % 4 or data.stride(0) % 4):
+        # only 8-bit plans with N % 4 == 0 stage rows by LDS-DMA (the others read global
+        # memory at any alignment)
+        if (data.element_size() == 1 and data.shape[1] % 4 == 0
+                and (data.data_ptr() % 4 or data.stride(0) % 4)):
             t = torch()
             with t.cuda.stream(stream if stream is not None else t.cuda.current_stream(data.device)):
                 return data.clone(memory_format=t.contiguous_format)
@@ -318,7 +324,9 @@ class Plan:
         info = np.zeros(len(INFO_FIELDS), np.int64)
         lib().pu_plan_info(self._h, info.ctypes.data_as(ctypes.c_void_p), len(INFO_FIELDS))
         d = dict(zip(INFO_FIELDS, info.tolist()))
-        return {"rechecked": d["cert_rechecked"], "nan_rule": bool(d["cert_nan"])}
+        return {"rechecked": d["cert_rechecked"], "nan_rule": bool(d["cert_nan"]),
+                "flagged_by": {"std": d["cert_std"], "sign": d["cert_sign"], "tie": d["cert_tie"]},
+                "settle_ms": d["cert_us"] / 1e3}
 
     def tile_window(self, tt):
         """Half-open sample range [a, b) (NOT reduced mod nsamples) time tile ``tt``
@@ -387,3 +395,24 @@ def series_stats(series, stream=None):
                                 ptr(out[3]), ctypes.c_void_p(ws.data_ptr() + off), wsb, stream_ptr(stream)),
           "pu_series_stats")
     return out
+
+
+class MaskedStream:
+    """A torch view of a CU-masked HIP stream (pu_stream_create_cu_masked) that leaves
+    ``reserve`` CUs free for kernels of other streams (RCCL during the chunked
+    broadcast).  Destroyed with the object."""
+
+    def __init__(self, reserve, device=None):
+        t = require_gpu()
+        h = ctypes.c_void_p()
+        with t.cuda.device(device if device is not None else t.cuda.current_device()):
+            check(lib().pu_stream_create_cu_masked(int(reserve), ctypes.byref(h)), "pu_stream_create_cu_masked")
+            self.stream = t.cuda.ExternalStream(h.value)
+        self._h = h
+        self.reserve = int(reserve)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib is not None:
+            _lib.pu_stream_destroy(h)
+            self._h = None

@@ -78,16 +78,25 @@ def channel_means_device(x):
     """``x.mean(1)`` with numpy's dtype and summation order (float32 stays float32).
 
     The last result is kept for the same tensor object while it is unmodified (its
-    version counter unchanged): get_noisier_channels and measure_channel_variability
-    both start from the channel means of one block, and the second call then skips a
-    pass over it.  A weak reference, so the cache never keeps a block alive."""
+    version counter and storage pointer unchanged): get_noisier_channels and
+    measure_channel_variability both start from the channel means of one block, and the
+    second call then skips a pass over it.  A weak reference, so the cache never keeps a
+    block alive; callers get a copy, so changing a result never changes the cache.
+    Writes that bypass torch's version counter (raw-pointer kernels, DLPack aliases)
+    are not seen: call :func:`invalidate_channel_means` after such a write (numpy inputs
+    are copied to a fresh tensor per call and never hit the cache)."""
     import weakref
     c = _MEANS[0]
-    if c is not None and c[0]() is x and c[1] == x._version:
-        return c[2]
+    if c is not None and c[0]() is x and c[1] == (x._version, x.data_ptr()):
+        return c[2].clone()
     m = _row_sums(x, 0, divisor=x.shape[1])
-    _MEANS[0] = (weakref.ref(x), x._version, m)
-    return m
+    _MEANS[0] = (weakref.ref(x), (x._version, x.data_ptr()), m)
+    return m.clone()
+
+
+def invalidate_channel_means():
+    """Forget the cached channel means (see :func:`channel_means_device`)."""
+    _MEANS[0] = None
 
 
 def channel_variances_device(x, means=None):

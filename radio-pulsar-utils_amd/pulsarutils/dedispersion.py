@@ -127,7 +127,7 @@ def _prepare_data(data):
 _PLAN_CACHE = collections.OrderedDict()
 _PLAN_CACHE_SIZE = 4
 _PLAN_LOCK = threading.Lock()
-_PLAN_ENV = ("PU_SUB_SHAPE", "PU_LDS_BUDGET_KB", "PU_GROUP", "PU_U8_DMA", "PU_SUB_SKIP")
+_PLAN_ENV = ("PU_SUB_SHAPE", "PU_LDS_BUDGET_KB", "PU_GROUP", "PU_U8_DMA")
 
 
 def _plan_for(x, shifts, acc, ident=None):
@@ -211,10 +211,19 @@ def dedispersion_search(data, dmmin, dmmax, start_freq, bandwidth, sample_time, 
                                                 acc=acc)
         return make_table({"DM": trial_DMs, "max": mx, "std": sd, "snr": snr, "rebin": win})
     x = _prepare_data(data)
+    if x.shape[1] < 8:
+        raise ValueError("zero-size array to reduction operation maximum which has no identity "
+                         f"(nsamples {x.shape[1]} < 8)")
     sh = _hip.shift_table(nchan, trial_DMs, start_freq, bandwidth, sample_time)
     plan = _plan_for(x, sh, _acc_code(acc or "f64"))
-    mx, sd, snr, win = plan.search(x)
     plane = plan.dedisperse(x)
+    if plane.dtype == _hip.torch().float64:
+        # the reference's serial path computes each row's statistics from the plane
+        # (dedispersion.py:223-243): pu_series_stats does that in numpy's order, so the
+        # table is bit-identical to the reference's with the (default) float64 plane
+        mx, sd, snr, win = _hip.series_stats(plane)
+    else:
+        mx, sd, snr, win = plan.search(x)
     table = make_table({"DM": trial_DMs, "max": _numpy_out(mx), "std": _numpy_out(sd), "snr": _numpy_out(snr),
                         "rebin": _numpy_out(win).astype(np.int64)})
     return table, _numpy_out(plane).astype(np.float64, copy=False)

@@ -59,38 +59,88 @@ def ready_tiles(plan, landed):
     return (starts + a0 >= 0) & (starts + b0 <= landed)
 
 
-def pipelined_broadcast_search(data, plan, out=None, workspace=None, src=0, chunks=8, group=None):
+class PlanSearcher:
+    """The per-rank work of :func:`pipelined_broadcast_search` on a HIP plan: time-tile
+    range searches as columns land (pu_plan_search_tiles), then pu_plan_finalize."""
+
+    def __init__(self, plan, out=None, workspace=None, device=None):
+        self.plan = plan
+        self.out, self.workspace = plan._outs_ws(device, out, workspace)
+        self.ntiles = plan.info["time_tiles"]
+
+    def ready(self, landed):
+        return ready_tiles(self.plan, landed)
+
+    def tiles(self, data, begin, end, stream=None):
+        self.plan.search_tiles(data, begin, end, self.workspace, stream=stream)
+
+    def finalize(self, data, stream=None):
+        return self.plan.finalize(self.workspace, data, out=self.out, stream=stream)
+
+    def streams_done(self, stream):
+        self.workspace.record_stream(stream)
+        for o in self.out:
+            o.record_stream(stream)
+
+
+def pipelined_broadcast_search(data, plan, out=None, workspace=None, src=0, chunks=8, group=None, searcher=None,
+                               reserve_cus=8):
     """Broadcast ``data`` from ``src`` in time chunks while searching it with ``plan``.
 
     Chunk k (a range of whole time tiles, all channels) is packed into a contiguous
-    staging buffer on ``src``, RCCL-broadcast on a communication stream and unpacked
+    staging buffer on ``src``, broadcast (RCCL on a communication stream) and unpacked
     into ``data`` on the other ranks; every time tile whose read window has landed is
-    searched on a compute stream as soon as its chunk's event fires
+    searched (on a compute stream) as soon as its chunk's event fires
     (pu_plan_search_tiles), and the per-trial outputs are finalised when all tiles ran
     (pu_plan_finalize).  Returns the (max, std, snr, rebin) device tensors; the caller's
     current stream is ordered after all of it.  ``plan=None`` (a rank with no trials)
     only takes part in the broadcasts.
+
+    While chunks are still to come, the tile searches go to a CU-masked stream that
+    leaves ``reserve_cus`` CUs to the broadcast's kernels (pu_stream_create_cu_masked;
+    0 = no mask); the tiles that wait for the last chunk and the finalize run unmasked.
+
+    ``searcher`` replaces the HIP work (an object with ``ntiles``, ``ready(landed)``,
+    ``tiles(data, begin, end, stream)`` and ``finalize(data, stream)``): with a CPU
+    ``data`` tensor the same chunk / staging / unpack / ready-tile sequence runs
+    synchronously, which is how the gloo tests drive the multi-rank branch on CPU.
     """
+    import contextlib
+
     import torch
     import torch.distributed as dist
+    cuda = data.is_cuda
     dev = data.device
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
+    if cuda and data.element_size() == 1 and data.shape[1] % 4 == 0 and (data.data_ptr() % 4 or data.stride(0) % 4):
+        # 8-bit LDS-DMA plans need dword-aligned rows; data is the receive buffer
+        raise ValueError("pipelined search of 8-bit data needs rows starting on 4-byte boundaries")
     nchan, n = data.shape
     bounds = column_chunks(n, chunks)
-    cur = torch.cuda.current_stream(dev)
-    comm = torch.cuda.Stream(device=dev)
-    comp = torch.cuda.Stream(device=dev)
-    comm.wait_stream(cur)
-    comp.wait_stream(cur)
-    if plan is not None:
-        out, workspace = plan._outs_ws(dev, out, workspace)
-        workspace.record_stream(comp)
-        done = np.zeros(plan.info["time_tiles"], dtype=bool)
+    if searcher is None and plan is not None:
+        searcher = PlanSearcher(plan, out, workspace, dev)
+    masked = None
+    if cuda:
+        cur = torch.cuda.current_stream(dev)
+        comm = torch.cuda.Stream(device=dev)
+        comp = torch.cuda.Stream(device=dev)
+        comm.wait_stream(cur)
+        comp.wait_stream(cur)
+        if world > 1 and reserve_cus > 0 and searcher is not None and len(bounds) > 1:
+            from ._hip import MaskedStream
+            masked = MaskedStream(reserve_cus, dev)
+            masked.stream.wait_stream(cur)
+    else:
+        cur = comm = comp = None
+    on_comm = (lambda: torch.cuda.stream(comm)) if cuda else contextlib.nullcontext
+    done = np.zeros(searcher.ntiles, dtype=bool) if searcher is not None else None
     width = max(c1 - c0 for c0, c1 in bounds)
     staging = torch.empty(nchan * width, dtype=data.dtype, device=dev) if world > 1 else None
-    for c0, c1 in bounds:
-        with torch.cuda.stream(comm):
+    for k, (c0, c1) in enumerate(bounds):
+        # tiles launched while later chunks are in flight use the masked stream
+        tstream = masked.stream if masked is not None and k + 1 < len(bounds) else comp
+        with on_comm():
             if world > 1:
                 buf = staging[:nchan * (c1 - c0)].view(nchan, c1 - c0)  # contiguous
                 if rank == src:
@@ -98,29 +148,40 @@ def pipelined_broadcast_search(data, plan, out=None, workspace=None, src=0, chun
                 dist.broadcast(buf, src=src, group=group)
                 if rank != src:
                     data[:, c0:c1].copy_(buf)
-            ev = torch.cuda.Event()
-            ev.record(comm)
-        if plan is None:
+            ev = None
+            if cuda:
+                ev = torch.cuda.Event()
+                ev.record(comm)
+        if searcher is None:
             continue
-        comp.wait_event(ev)
-        ready = ready_tiles(plan, c1) & ~done
+        if cuda:
+            tstream.wait_event(ev)
+        ready = searcher.ready(c1) & ~done
         idx = np.flatnonzero(ready)
         # contiguous runs of ready tiles, one launch each
         for run in np.split(idx, np.flatnonzero(np.diff(idx) != 1) + 1) if idx.size else []:
-            plan.search_tiles(data, int(run[0]), int(run[-1]) + 1, workspace, stream=comp)
+            searcher.tiles(data, int(run[0]), int(run[-1]) + 1, stream=tstream)
         done |= ready
-    if staging is not None:
-        staging.record_stream(comm)
-    cur.wait_stream(comm)
-    if plan is None:
+        if masked is not None and k + 2 == len(bounds):
+            comp.wait_stream(masked.stream)  # the unmasked stream takes over for the last chunk
+    if cuda:
+        if staging is not None:
+            staging.record_stream(comm)
+        cur.wait_stream(comm)
+    if searcher is None:
         return None
     if not done.all():
         raise RuntimeError("pipelined search: time tiles left unsearched")
-    plan.finalize(workspace, data, out=out, stream=comp)
-    for o in out:
-        o.record_stream(comp)
-    cur.wait_stream(comp)
-    return out
+    res = searcher.finalize(data, stream=comp)
+    if cuda:
+        if hasattr(searcher, "streams_done"):
+            searcher.streams_done(comp)
+            if masked is not None:
+                searcher.streams_done(masked.stream)
+        cur.wait_stream(comp)
+        if masked is not None:
+            masked.stream.synchronize()  # before the stream is destroyed with ``masked``
+    return res
 
 
 def sharded_search(data, trial_DMs, nchan, start_freq, bandwidth, sample_time, group=None, acc=None,

@@ -24,7 +24,7 @@ fi
 if [ -n "$ABLATE" ]; then
   for sk in $ABLATE; do
     echo "skip=$sk" >> gpurun_out/${TAG}_ablate.log
-    PU_SUB_SKIP=$sk PU_ROUNDS=1 PU_SWEEP=${ABLATE_VARIANT:-4:160:0} timeout -k 10 200 python3 scripts/sweep.py C2 >> gpurun_out/${TAG}_ablate.log 2>&1 || exit $?
+    PULSARUTILS_HIP_LIB=radio-pulsar-utils_amd/pulsarutils/_lib/libpulsarutils_hip_stamps.so PU_SUB_SKIP=$sk PU_ROUNDS=1 PU_SWEEP=${ABLATE_VARIANT:-4:160:0} timeout -k 10 200 python3 scripts/sweep.py C2 >> gpurun_out/${TAG}_ablate.log 2>&1 || exit $?
   done
 fi
 if [ -n "$CLEANSWEEP" ]; then

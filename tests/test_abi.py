@@ -3,6 +3,8 @@ import ctypes
 import os
 import re
 
+import pytest
+
 from conftest import REPO
 
 
@@ -36,3 +38,17 @@ def test_error_path_without_gpu():
     rc = _hip.lib().pu_plan_create(ctypes.byref(h), 7, 0, 4, 16, None, 1)
     assert rc == -1
     assert "unsupported dtype" in _hip.lib().pu_last_error().decode()
+
+
+def test_m0_consumers_checked_on_device_code():
+    """the slot build leaves its M0 behind; no other M0 consumer of the subband
+    kernels may read it (scripts/check_m0.py on the assembly the production compile keeps)."""
+    import subprocess
+    import sys
+    asm = os.path.join(REPO, "radio-pulsar-utils_amd", "csrc", "dedisperse-hip-amdgcn-amd-amdhsa-gfx950.s")
+    if not os.path.exists(asm):
+        pytest.skip("device assembly not built here (make -C radio-pulsar-utils_amd/csrc)")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "scripts", "check_m0.py"), asm],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert " 0 reading" in r.stdout, r.stdout

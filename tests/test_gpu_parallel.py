@@ -81,3 +81,48 @@ def test_sharded_search_nccl_world1(gpu, pipelined):
     np.testing.assert_allclose(snr[idx], o[2], rtol=1e-5)
     np.testing.assert_array_equal(win[idx], o[3])
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("offset", [0, 5000])
+@pytest.mark.parametrize("dt", ["f32", "u8dma", "u8", "f64"])
+def test_ready_tiles_read_only_landed_columns(gpu, dt, offset):
+    """the halo that gates early tile launches (Plan.tile_window) is checked
+    against the kernels' real reads.  Every chunk's not-yet-landed columns are
+    overwritten with garbage (NaN / 255) before the tiles ``ready_tiles`` marks are
+    searched; the finalised result must equal the one-shot search bit for bit, so no
+    ready tile may read past the landed prefix.  Plans: float32 (LDS-DMA rows), 8-bit
+    with LDS-DMA rows (N % 4 == 0) and with global-memory rows (N % 4 != 0), float64
+    (channel mode); shift tables with a negative (offset 0: the reference's delays
+    around the band centre) and a positive smallest shift (offset 5000)."""
+    import torch
+    c = CONFIGS["C2"]
+    nchan = 96
+    n = 40962 if dt == "u8" else 40960
+    rng = np.random.default_rng(17)
+    xh = rng.random((nchan, n)) * 40
+    x = torch.from_numpy({"f32": xh.astype(np.float32), "u8dma": xh.astype(np.uint8), "u8": xh.astype(np.uint8),
+                          "f64": xh}[dt]).cuda()
+    dms = np.linspace(0.0, 80.0, 150)
+    sh = _hip.shift_table(nchan, dms, c.start_freq, c.bandwidth, c.tsamp) + offset
+    assert (sh.min() < 0) == (offset == 0)
+    plan = _hip.Plan(_hip.dtype_code(x.dtype), _hip.PU_ACC_NATIVE, nchan, n, sh)
+    full = [o.cpu().numpy() for o in plan.search(x)]
+    ws = torch.empty(plan.workspace_bytes, dtype=torch.uint8, device=x.device)
+    done = np.zeros(plan.info["time_tiles"], dtype=bool)
+    launched = 0
+    for c0, c1 in parallel.column_chunks(n, 6):
+        xg = x.clone()
+        if c1 < n:
+            xg[:, c1:] = 255 if x.dtype == torch.uint8 else float("nan")
+        ready = parallel.ready_tiles(plan, c1) & ~done
+        idx = np.flatnonzero(ready)
+        for run in np.split(idx, np.flatnonzero(np.diff(idx) != 1) + 1) if idx.size else []:
+            plan.search_tiles(xg, int(run[0]), int(run[-1]) + 1, ws)
+            launched += 1
+        done |= ready
+        torch.cuda.synchronize()
+        del xg
+    assert done.all() and launched > 1
+    got = [o.cpu().numpy() for o in plan.finalize(ws, x)]
+    for a, b in zip(full, got):
+        np.testing.assert_array_equal(a, b)

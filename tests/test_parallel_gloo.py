@@ -131,3 +131,85 @@ def test_ready_tiles_halo(shift_min, shift_max):
     assert seen.all()
     if shift_min < 0:
         assert not ready_tiles(plan, n - 1)[0]  # tile 0 wraps to the end of the array
+
+
+PIPE_WORKER = textwrap.dedent("""
+    import sys
+    sys.path[:0] = [{pkg!r}, {repo!r}]
+    import numpy as np, torch, torch.distributed as dist
+    from pulsarutils._hip import Plan
+    from pulsarutils.parallel import pipelined_broadcast_search, ready_tiles
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    nchan, n, tt_len = 6, {n}, 512
+    full = (np.random.default_rng(3).random((nchan, n)) * 100).astype({dtype!r})
+    data = torch.from_numpy(full.copy()) if rank == {src} else torch.zeros((nchan, n), dtype=torch.from_numpy(full).dtype)
+
+    class FakePlan:
+        nsamples = n
+        info = {{"time_tile": tt_len, "time_tiles": -(-n // tt_len), "max_spread": 74}}
+        shift_min, shift_max = {smin}, {smax}
+        def tile_window(self, tt):
+            return Plan.tile_window(self, tt)
+
+    class CheckSearcher:
+        # every searched tile's read window must already hold the source's columns
+        def __init__(self):
+            self.plan = FakePlan()
+            self.ntiles = self.plan.info["time_tiles"]
+            self.count = np.zeros(self.ntiles, dtype=int)
+        def ready(self, landed):
+            return ready_tiles(self.plan, landed)
+        def tiles(self, d, b, e, stream=None):
+            assert stream is None
+            for tt in range(b, e):
+                a0, b0 = self.plan.tile_window(tt)
+                cols = np.arange(a0, b0) % n
+                assert np.array_equal(d[:, cols].numpy(), full[:, cols]), (rank, tt)
+                self.count[tt] += 1
+        def finalize(self, d, stream=None):
+            assert (self.count == 1).all(), self.count
+            return "finalized"
+
+    s = CheckSearcher()
+    assert pipelined_broadcast_search(data, None, src={src}, chunks={chunks}, searcher=s) == "finalized"
+    assert np.array_equal(data.numpy(), full)
+    dist.barrier()
+    dist.destroy_process_group()
+    print("rank", rank, "ok")
+""")
+
+
+@pytest.mark.parametrize("world,src,n,chunks,smin,smax,dtype", [
+    (2, 0, 50000, 5, -2084, 2914, "float32"),
+    (3, 1, 1 << 16, 8, 0, 582, "uint8"),
+    (4, 3, 40962, 3, -843, 1931, "float64"),
+    (2, 1, 9000, 8, 100, 700, "uint8"),
+])
+def test_pipelined_broadcast_gloo(tmp_path, world, src, n, chunks, smin, smax, dtype):
+    """The multi-rank branch of parallel.pipelined_broadcast_search (staging pack on the
+    source, chunk broadcast, unpack on the others, ready-tile launches) on CPU under gloo
+    at world 2-4 with any source rank: every time tile is searched exactly once, only
+    after every column of its read window holds the source's data, and the landed data
+    equals the source on every rank at the end."""
+    script = tmp_path / "pipe_worker.py"
+    script.write_text(PIPE_WORKER.format(pkg=PKG_DIR, repo=REPO, n=n, src=src, chunks=chunks, smin=smin, smax=smax,
+                                         dtype=dtype))
+    port = _free_port()
+    procs = []
+    for rank in range(world):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                   LOCAL_RANK=str(rank), OMP_NUM_THREADS="1")
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out, _ = p.communicate()
+        outs.append(out)
+    for p, out in zip(procs, outs):
+        assert p.returncode == 0, out
+        assert "ok" in out
