@@ -114,9 +114,15 @@ __global__ void exact_final_kernel(int64_t rows, int64_t n, const uint64_t *__re
 
 // The reference's dedispersed series of a few trials, directly: out[r][t] =
 // ((0 + x[0][(t + s[r][0]) mod n]) + x[1][...]) + ... in float64, channel order
-// (roll_and_sum's order, dedispersion.py:60-98: bit-identical).  Each thread owns 4
-// consecutive samples; a wave reads 256 consecutive elements of a row per channel.  The
-// row shifts (in [0, n)) go through LDS 1024 channels at a time.
+// (roll_and_sum's order, dedispersion.py:60-98: bit-identical).  The row shifts (in
+// [0, n)) go through LDS 1024 channels at a time.  Every trial reads the whole input
+// once (17 GB at C3: ~4 ms), which is why only flagged trials take this path.
+//   8-bit: a thread owns 8 consecutive samples and reads them as 3 aligned dwords
+//   (lanes 32 B apart: coalesced), bytes extracted by funnel shifts;
+//   float: a thread owns samples t0 + l + 64 k (k < 8): every load of a wave is 64
+//   consecutive elements.
+constexpr int kSeriesPer = 8;
+
 template <typename T>
 __global__ void __launch_bounds__(256)
 exact_series_kernel(const T *__restrict__ x, int64_t ld, int64_t nchan, int64_t n, const int64_t *__restrict__ shifts,
@@ -124,28 +130,52 @@ exact_series_kernel(const T *__restrict__ x, int64_t ld, int64_t nchan, int64_t 
 {
     __shared__ int64_t sh[1024];
     const int64_t r = blockIdx.y;
-    const int64_t t0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // the wave's 512 samples start at w0; this thread's samples
+    const int64_t w0 = ((int64_t)blockIdx.x * 4 + wave) * 64 * kSeriesPer;
+    const int64_t t0 = sizeof(T) == 1 ? w0 + (int64_t)kSeriesPer * lane : w0 + lane;
+    const int64_t dt = sizeof(T) == 1 ? 1 : 64;  // sample step between this thread's samples
+    double acc[kSeriesPer];
+#pragma unroll
+    for (int k = 0; k < kSeriesPer; ++k) acc[k] = 0.0;
     for (int64_t c0 = 0; c0 < nchan; c0 += 1024) {
         const int64_t nc = nchan - c0 < 1024 ? nchan - c0 : 1024;
         __syncthreads();
         for (int64_t i = threadIdx.x; i < nc; i += 256) sh[i] = shifts[r * nchan + c0 + i];
         __syncthreads();
-        if (t0 >= n) continue;
+        if (w0 >= n) continue;
         for (int64_t ci = 0; ci < nc; ++ci) {
             const T *row = x + (c0 + ci) * ld;
             int64_t idx = t0 + sh[ci];
             if (idx >= n) idx -= n;
+            if constexpr (sizeof(T) == 1) {
+                const bool fast = idx + 12 <= n && t0 + kSeriesPer <= n && (reinterpret_cast<uintptr_t>(row) & 3) == 0;
+                if (fast) {
+                    const int64_t a = idx & ~int64_t(3);
+                    const uint32_t *p = reinterpret_cast<const uint32_t *>(row + a);
+                    const uint32_t d0 = p[0], d1 = p[1], d2 = p[2];
+                    const uint32_t sft = (uint32_t)(idx - a) * 8u;
+                    // bytes idx .. idx + 7 as two dwords (funnel shift across the dwords)
+                    const uint32_t lo = sft ? (d0 >> sft) | (d1 << (32u - sft)) : d0;
+                    const uint32_t hi = sft ? (d1 >> sft) | (d2 << (32u - sft)) : d1;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (t0 + k < n) acc[k] += static_cast<double>(row[idx]);
-                if (++idx == n) idx = 0;
+                    for (int k = 0; k < 4; ++k) acc[k] += (double)((lo >> (8 * k)) & 0xffu);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) acc[4 + k] += (double)((hi >> (8 * k)) & 0xffu);
+                    continue;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kSeriesPer; ++k) {
+                if (t0 + k * dt < n) acc[k] += static_cast<double>(row[idx]);
+                idx += dt;
+                while (idx >= n) idx -= n;  // n < 64 may wrap more than once
             }
         }
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-        if (t0 + k < n) out[r * n + t0 + k] = acc[k];
+    for (int k = 0; k < kSeriesPer; ++k)
+        if (t0 + k * dt < n) out[r * n + t0 + k * dt] = acc[k];
 }
 
 template <typename T>
@@ -271,7 +301,7 @@ int nonfinite_any_async(const void *data, int dtype, int64_t nrows, int64_t n, i
 int exact_series(const void *data, int dtype, int64_t nchan, int64_t n, int64_t ld, const int64_t *shifts, int64_t rows,
                  double *out, hipStream_t s)
 {
-    const dim3 grid((unsigned)((n + 1023) / 1024), (unsigned)rows), blk(256);
+    const dim3 grid((unsigned)((n + 4 * 64 * kSeriesPer - 1) / (4 * 64 * kSeriesPer)), (unsigned)rows), blk(256);
     switch (dtype) {
     case PU_U8:
         hipLaunchKernelGGL(exact_series_kernel<uint8_t>, grid, blk, 0, s, reinterpret_cast<const uint8_t *>(data), ld,

@@ -84,7 +84,7 @@ class PlanSearcher:
 
 
 def pipelined_broadcast_search(data, plan, out=None, workspace=None, src=0, chunks=8, group=None, searcher=None,
-                               reserve_cus=8):
+                               reserve_cus=0):
     """Broadcast ``data`` from ``src`` in time chunks while searching it with ``plan``.
 
     Chunk k (a range of whole time tiles, all channels) is packed into a contiguous
@@ -96,9 +96,13 @@ def pipelined_broadcast_search(data, plan, out=None, workspace=None, src=0, chun
     current stream is ordered after all of it.  ``plan=None`` (a rank with no trials)
     only takes part in the broadcasts.
 
-    While chunks are still to come, the tile searches go to a CU-masked stream that
-    leaves ``reserve_cus`` CUs to the broadcast's kernels (pu_stream_create_cu_masked;
-    0 = no mask); the tiles that wait for the last chunk and the finalize run unmasked.
+    ``reserve_cus`` > 0: while chunks are still to come, the tile searches go to a
+    CU-masked stream that leaves that many CUs to the broadcast's kernels
+    (pu_stream_create_cu_masked); the tiles that wait for the last chunk and the
+    finalize run unmasked.  Off by default: on one MI355X the proxy
+    (scripts/overlap_probe.py, profiles/r03/overlap_probe_r3b.json) shows copy kernels on
+    a second stream getting 2.2 TB/s beside the unmasked search, and an 8-CU mask slowing
+    the search alone by 15 % (15.6 -> 18.0 ms) without speeding the copies.
 
     ``searcher`` replaces the HIP work (an object with ``ntiles``, ``ready(landed)``,
     ``tiles(data, begin, end, stream)`` and ``finalize(data, stream)``): with a CPU

@@ -10,6 +10,8 @@
 //   r2st64 : each window as 2 x ds_read2st64_b64
 //   b128   : each window as 2 x ds_read_b128 (16 B per lane, 16-B aligned)
 //   b128m8 : the same at addresses 8 B off the 16-B alignment
+//   r2b32  : each window as 4 x ds_read2_b32 (8-B aligned), and 4 B off alignment
+//   b64m4  : 4 x ds_read_b64 4 B off alignment
 // Adds are v_pk_add_f32 (4 per window), as in the kernel.
 // Build: hipcc --offload-arch=gfx950 -O3 -o scripts/lds_probe scripts/lds_probe.hip
 #include <hip/hip_runtime.h>
@@ -41,7 +43,24 @@ __global__ void __launch_bounds__(1024) lds_kernel(float *out, const unsigned *o
                  : "=&v"(W[0]), "=&v"(W[1]), "=&v"(W[2]), "=&v"(W[3])                                    \
                  : "v"(A)                                                                              \
                  : "memory");
-        if constexpr (MODE >= 5) {
+        if constexpr (MODE >= 9) {
+            // 9: ds_read2_b32 pairs at the 8-B aligned window addresses; 10: the same 4 B off
+            // (an odd window of a single-copy slot); 11: ds_read_b64 4 B off alignment
+            const uint32_t mo = MODE == 9 ? 0u : 4u;
+            const uint32_t b0 = a0 + mo, b1 = a1 + mo, b2 = a2 + mo;
+#define RD2W(W, A)                                                                                     \
+    if constexpr (MODE == 11)                                                                          \
+        asm volatile("ds_read_b64 %0, %4\n\tds_read_b64 %1, %4 offset:512\n\t"                            \
+                     "ds_read_b64 %2, %4 offset:1024\n\tds_read_b64 %3, %4 offset:1536"                    \
+                     : "=&v"(W[0]), "=&v"(W[1]), "=&v"(W[2]), "=&v"(W[3]) : "v"(A) : "memory");           \
+    else                                                                                               \
+        asm volatile("ds_read2_b32 %0, %4 offset1:1\n\tds_read2_b32 %1, %4 offset0:128 offset1:129\n\t"  \
+                     "ds_read2_b32 %2, %5 offset1:1\n\tds_read2_b32 %3, %5 offset0:128 offset1:129"        \
+                     : "=&v"(W[0]), "=&v"(W[1]), "=&v"(W[2]), "=&v"(W[3]) : "v"(A), "v"(A + 1024u) : "memory");
+            RD2W(w[0], b0) RD2W(w[1], b1) RD2W(w[2], b2)
+#undef RD2W
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w[0][0]), "+v"(w[1][0]), "+v"(w[2][0]) : : "memory");
+        } else if constexpr (MODE >= 5) {
             const uint32_t mo = MODE == 8 ? 8u : 0u;
             const uint32_t b0 = MODE >= 7 ? a0 + 8u * lane + mo : a0, b1 = MODE >= 7 ? a1 + 8u * lane + mo : a1,
                            b2 = MODE >= 7 ? a2 + 8u * lane + mo : a2;
@@ -86,7 +105,7 @@ __global__ void __launch_bounds__(1024) lds_kernel(float *out, const unsigned *o
             RD4(w[2], a2)
         }
 #undef RD4
-        if constexpr (MODE < 5)
+        if constexpr (MODE < 5 || MODE >= 9)
             asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w[0][0]), "+v"(w[1][0]), "+v"(w[2][0]) : : "memory");
 #pragma unroll
         for (int q = 0; q < 3; ++q)
@@ -140,7 +159,10 @@ int main()
         hipFuncSetAttribute((const void *)lds_kernel<5>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536) ||
         hipFuncSetAttribute((const void *)lds_kernel<6>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536) ||
         hipFuncSetAttribute((const void *)lds_kernel<7>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536) ||
-        hipFuncSetAttribute((const void *)lds_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536))
+        hipFuncSetAttribute((const void *)lds_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536) ||
+        hipFuncSetAttribute((const void *)lds_kernel<9>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536) ||
+        hipFuncSetAttribute((const void *)lds_kernel<10>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536) ||
+        hipFuncSetAttribute((const void *)lds_kernel<11>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536))
         return 2;
     printf("full (12 reads):\n");
     run(lds_kernel<0>, out, offs, blocks, 12);
@@ -160,6 +182,12 @@ int main()
     run(lds_kernel<7>, out, offs, blocks, 12);
     printf("2 x ds_read_b128 per window, 8 B off alignment:\n");
     run(lds_kernel<8>, out, offs, blocks, 12);
+    printf("4 x ds_read2_b32 per window (8-B aligned):\n");
+    run(lds_kernel<9>, out, offs, blocks, 12);
+    printf("4 x ds_read2_b32 per window, 4 B off alignment:\n");
+    run(lds_kernel<10>, out, offs, blocks, 12);
+    printf("4 x ds_read_b64 per window, 4 B off alignment:\n");
+    run(lds_kernel<11>, out, offs, blocks, 12);
     printf("(LDS peak 157.3 TB/s = 256 CU x 256 B/clk x 2.4 GHz)\n");
     const hipError_t e = hipDeviceSynchronize();
     printf("status %s\n", hipGetErrorString(e));
