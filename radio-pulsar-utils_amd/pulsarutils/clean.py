@@ -194,9 +194,10 @@ def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=
     if badchans_mask is None:
         badchans_mask = np.zeros(nchan, dtype=bool)
     bad_np = np.ascontiguousarray(np.asarray(badchans_mask, dtype=bool)).astype(np.uint8)
-    # host->device copies first: a pageable copy synchronises the stream, so none may
-    # sit between two kernels of the pass
-    bad = t.from_numpy(bad_np).to(dev)
+    # the mask goes through pinned memory asynchronously: a pageable copy would block
+    # the host until the stream drained (the previous call's kernels), so the next
+    # call's launches could not queue behind them
+    bad = t.from_numpy(bad_np).pin_memory().to(dev, non_blocking=True)
     sigma = min(baseline_window, n // 100 * 2 + 1)
     dw, radius = _gaussian_weights_device(sigma, dev)
     lc = t.empty(n, dtype=t.float64, device=dev)
@@ -307,7 +308,7 @@ def dm_broadening(dm, freq, df):
 
 
 def search_by_chunks(fname, chunk_length=None, new_sample_time=None, tmin=0, dmmin=200, dmmax=800, surelybad=[],
-                     save_candidates=True, snr_threshold=6, acc=None, search_dtype="f32", profile=None,
+                     save_candidates=True, snr_threshold=6, acc=None, search_dtype="f64", profile=None,
                      zero_dm=False):
     """clean.py:276-351: stream a SIGPROC file through clean + DM search, chunk by chunk.
 
@@ -319,11 +320,12 @@ def search_by_chunks(fname, chunk_length=None, new_sample_time=None, tmin=0, dmm
     ``N = rint(new_sample_time / tsamp)`` when >= 2; ``dedispersion_search``.  All array
     work stays in HBM (read_block_device -> renormalize_device -> HIP rebin -> search).
 
-    ``search_dtype``: the renormalised chunk is float64 (clean.py:73); ``"f32"``
-    (default) casts it to float32 on the device and searches with the float32 subband
-    kernel (the north star's float32 summation-order tolerance), ``"f64"`` searches the
-    float64 plane with float64 accumulation in channel order (bit-exact series, the
-    slower channel-mode kernel).  ``zero_dm`` is renormalize_data's opt-in subtraction.
+    ``search_dtype``: the renormalised chunk is float64 (clean.py:73); ``"f64"``
+    (default, the reference's behaviour, clean.py:346) searches it with float64
+    accumulation in channel order (bit-exact series; certified statistics), ``"f32"``
+    casts it to float32 on the device and searches with the float32 subband kernel (the
+    north star's float32 summation-order tolerance; ~3x faster per chunk, but the file
+    pipeline is bound by the host read + PCIe copy either way).  ``zero_dm`` is renormalize_data's opt-in subtraction.
     ``profile``: a list that receives one dict of synchronised per-step timings (ms:
     h2d, transpose, clean, cast, rebin, search) per chunk.
 

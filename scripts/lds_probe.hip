@@ -118,6 +118,85 @@ __global__ void __launch_bounds__(1024) lds_kernel(float *out, const unsigned *o
     out[blockIdx.x * 1024 + threadIdx.x] = t;
 }
 
+// Width probes: MODE 0 = 8 x ds_read_b32, 1 = 4 x ds_read_b64 (same bytes), 2 = 8 x
+// ds_write_addtid_b32 (M0 set once), 3 = 4 x ds_write_b64 (same bytes), 4 = 8 x ds_write_b32.
+template <int MODE>
+__global__ void __launch_bounds__(1024) width_kernel(float *out, const unsigned *offs)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char *)smem;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float acc = 0.0f;
+    const uint32_t wbase = base + (uint32_t)wave * 4096u;  // 4 KiB per wave
+    for (int it = 0; it < kIters; ++it) {
+        const unsigned o = __builtin_amdgcn_readfirstlane(offs[it & 255]) & 0x3f00u;  // 256-B aligned
+        if constexpr (MODE == 0) {
+            const uint32_t a = base + o + 4u * lane;
+            float v[8];
+            asm volatile("ds_read_b32 %0, %8\n\tds_read_b32 %1, %8 offset:256\n\tds_read_b32 %2, %8 offset:512\n\t"
+                         "ds_read_b32 %3, %8 offset:768\n\tds_read_b32 %4, %8 offset:1024\n\t"
+                         "ds_read_b32 %5, %8 offset:1280\n\tds_read_b32 %6, %8 offset:1536\n\t"
+                         "ds_read_b32 %7, %8 offset:1792\n\ts_waitcnt lgkmcnt(0)"
+                         : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]),
+                           "=&v"(v[7]) : "v"(a) : "memory");
+            for (int k = 0; k < 8; ++k) acc += v[k];
+        } else if constexpr (MODE == 1) {
+            const uint32_t a = base + o + 8u * lane;
+            double v[4];
+            asm volatile("ds_read_b64 %0, %4\n\tds_read_b64 %1, %4 offset:512\n\tds_read_b64 %2, %4 offset:1024\n\t"
+                         "ds_read_b64 %3, %4 offset:1536\n\ts_waitcnt lgkmcnt(0)"
+                         : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]) : "v"(a) : "memory");
+            for (int k = 0; k < 4; ++k) acc += (float)v[k];
+        } else if constexpr (MODE == 2) {
+            const float x = (float)it;
+            asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                         "ds_write_addtid_b32 %0\n\tds_write_addtid_b32 %0 offset:256\n\t"
+                         "ds_write_addtid_b32 %0 offset:512\n\tds_write_addtid_b32 %0 offset:768\n\t"
+                         "ds_write_addtid_b32 %0 offset:1024\n\tds_write_addtid_b32 %0 offset:1280\n\t"
+                         "ds_write_addtid_b32 %0 offset:1536\n\tds_write_addtid_b32 %0 offset:1792\n\t"
+                         "s_waitcnt lgkmcnt(0)"
+                         : : "v"(x), "s"(__builtin_amdgcn_readfirstlane(wbase + (o & 0x300u))) : "memory");
+            acc += x;
+        } else if constexpr (MODE == 3) {
+            const double x = (double)it;
+            const uint32_t a = wbase + (o & 0x300u) + 8u * lane;
+            asm volatile("ds_write_b64 %1, %0\n\tds_write_b64 %1, %0 offset:512\n\tds_write_b64 %1, %0 offset:1024\n\t"
+                         "ds_write_b64 %1, %0 offset:1536\n\ts_waitcnt lgkmcnt(0)"
+                         : : "v"(x), "v"(a) : "memory");
+            acc += (float)x;
+        } else if constexpr (MODE == 5) {
+            // 8 x ds_read_u8 (one byte per lane each)
+            const uint32_t a = base + o + lane;
+            uint32_t v[8];
+            asm volatile("ds_read_u8 %0, %8\n\tds_read_u8 %1, %8 offset:64\n\tds_read_u8 %2, %8 offset:128\n\t"
+                         "ds_read_u8 %3, %8 offset:192\n\tds_read_u8 %4, %8 offset:256\n\t"
+                         "ds_read_u8 %5, %8 offset:320\n\tds_read_u8 %6, %8 offset:384\n\t"
+                         "ds_read_u8 %7, %8 offset:448\n\ts_waitcnt lgkmcnt(0)"
+                         : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]),
+                           "=&v"(v[7]) : "v"(a) : "memory");
+            for (int k = 0; k < 8; ++k) acc += (float)v[k];
+        } else if constexpr (MODE == 6) {
+            // 2 x ds_write_b128 (2 KiB per wave)
+            typedef float f4 __attribute__((ext_vector_type(4)));
+            const f4 x = {(float)it, 1.0f, 2.0f, 3.0f};
+            const uint32_t a = wbase + (o & 0x300u) * 0 + 16u * lane;
+            asm volatile("ds_write_b128 %1, %0\n\tds_write_b128 %1, %0 offset:1024\n\ts_waitcnt lgkmcnt(0)"
+                         : : "v"(x), "v"(a) : "memory");
+            acc += x.x;
+        } else {
+            const float x = (float)it;
+            const uint32_t a = wbase + (o & 0x300u) + 4u * lane;
+            asm volatile("ds_write_b32 %1, %0\n\tds_write_b32 %1, %0 offset:256\n\tds_write_b32 %1, %0 offset:512\n\t"
+                         "ds_write_b32 %1, %0 offset:768\n\tds_write_b32 %1, %0 offset:1024\n\t"
+                         "ds_write_b32 %1, %0 offset:1280\n\tds_write_b32 %1, %0 offset:1536\n\t"
+                         "ds_write_b32 %1, %0 offset:1792\n\ts_waitcnt lgkmcnt(0)"
+                         : : "v"(x), "v"(a) : "memory");
+            acc += x;
+        }
+    }
+    out[blockIdx.x * 1024 + threadIdx.x] = acc;
+}
+
 using Kern = void (*)(float *, const unsigned *);
 
 static double run(Kern k, float *out, const unsigned *offs, int blocks, double reads_per_iter)
@@ -188,6 +267,23 @@ int main()
     run(lds_kernel<10>, out, offs, blocks, 12);
     printf("4 x ds_read_b64 per window, 4 B off alignment:\n");
     run(lds_kernel<11>, out, offs, blocks, 12);
+    for (auto k : {width_kernel<0>, width_kernel<1>, width_kernel<2>, width_kernel<3>, width_kernel<4>,
+                   width_kernel<5>, width_kernel<6>})
+        if (hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, 65536)) return 3;
+    printf("width: 8 x ds_read_b32 (2 KiB per wave):\n");
+    run(width_kernel<0>, out, offs, blocks, 4);
+    printf("width: 4 x ds_read_b64 (2 KiB per wave):\n");
+    run(width_kernel<1>, out, offs, blocks, 4);
+    printf("width: 8 x ds_write_addtid_b32 (2 KiB per wave):\n");
+    run(width_kernel<2>, out, offs, blocks, 4);
+    printf("width: 4 x ds_write_b64 (2 KiB per wave):\n");
+    run(width_kernel<3>, out, offs, blocks, 4);
+    printf("width: 8 x ds_write_b32 (2 KiB per wave):\n");
+    run(width_kernel<4>, out, offs, blocks, 4);
+    printf("width: 8 x ds_read_u8 (512 B per wave; TB/s column is 4x the bytes moved):\n");
+    run(width_kernel<5>, out, offs, blocks, 4);
+    printf("width: 2 x ds_write_b128 (2 KiB per wave):\n");
+    run(width_kernel<6>, out, offs, blocks, 4);
     printf("(LDS peak 157.3 TB/s = 256 CU x 256 B/clk x 2.4 GHz)\n");
     const hipError_t e = hipDeviceSynchronize();
     printf("status %s\n", hipGetErrorString(e));
