@@ -711,6 +711,7 @@ struct SubArgs {
     int32_t dma_waves;      // waves that issue the LDS-DMA rows (the last ones of the workgroup)
     int32_t nitems;         // work items (DM tiles x time tiles of this launch)
     int32_t base_bits;      // DMA row words: base = word & (2^base_bits - 1), cover = (word >> base_bits) x 256 B
+    int32_t dt_major;       // item order: 0 = time tile major (DM tiles of a time tile share L2), 1 = DM tile major
     void *stamps;           // diagnostic build (PU_STAMPS): 8 x u64 phase-cycle totals
 };
 
@@ -888,8 +889,12 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
     typedef uint32_t rec_t __attribute__((ext_vector_type(D)));
     const DedispArgs &o = a.o;
     const int ndt = o.ndt;
-    const int dt = wg % ndt;
-    const int tt = o.tt0 + wg / ndt;
+    // Items in dispatch order.  The planner sorts the DM tiles by decreasing cost, so
+    // DM-tile-major order dispatches the longest items first (LPT: the short ones fill
+    // the tail), for grids of few items per CU; time-tile-major order keeps the DM tiles
+    // of one time tile together (one XCD, its L2 serving their overlapping rows).
+    const int dt = a.dt_major ? wg / o.ntt_run : wg % ndt;
+    const int tt = o.tt0 + (a.dt_major ? wg % o.ntt_run : wg / ndt);
     const int t0 = tt * TT;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1412,6 +1417,7 @@ struct pu_plan {
     size_t slot_bytes = 0, zero_len = 0;
     int64_t exec_adds = 0, lds_traffic = 0;  // per launch (measurement: bench.py roofline)
     int64_t nstages = 0;
+    int dt_major = 0;  // subband item order (SubArgs::dt_major)
     i32x4 *d_tiles = nullptr, *d_stages = nullptr;
     i32x2 *d_tile_stages = nullptr;
     int32_t *d_slots = nullptr;
@@ -1495,6 +1501,7 @@ int launch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
     const int64_t nitems = (int64_t)p->ndt * a.ntt_run;
     sa.nitems = (int32_t)nitems;
     sa.base_bits = p->base_bits;
+    sa.dt_major = p->dt_major;
     const int64_t nblk = nitems;
     const dim3 grid((unsigned)nblk), block(C::THREADS);
     auto go = [&](auto kern) {
@@ -1705,6 +1712,7 @@ int plan_channels(pu_plan *p, const int64_t *shifts, size_t budget)
 // trial's group does not fit the LDS budget (the caller then tries a smaller G, then
 // channel mode).
 constexpr int64_t kSubMaxSpread = 2048;
+constexpr int64_t kDtMajorItems = 16 * 256;  // below this many items per launch: DM-tile-major order
 
 struct SubSlot {
     int32_t vid;     // relative-shift vector id (per group)
@@ -1881,7 +1889,9 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     };
     int64_t slot_used = 0, max_stage_chans = 0;
     int64_t adds_tile = 0, lds_tile = 0;  // per time tile, summed over DM tiles
+    std::vector<double> tile_cost((size_t)ndt);  // per DM tile: LDS bytes + stage overhead (cost model)
     for (int t = 0; t < ndt; ++t) {
+        const int64_t lds_before = lds_tile;
         const int64_t cb = copy_of(span_t[t]);
         const int64_t *smin = smin_t.data() + (size_t)t * nchan;
         const int64_t *smax = smax_t.data() + (size_t)t * nchan;
@@ -1983,6 +1993,32 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
                 }
             }
         }
+        tile_cost[t] = (double)(lds_tile - lds_before) + 3.0e6 * tile_stages[t][1];
+    }
+    // DM tiles in decreasing cost order (the kernel's DM-tile-major item order then
+    // dispatches the longest items first).  A tile's trials are named by its record, so
+    // the order changes nothing else.
+    {
+        std::vector<int> perm((size_t)ndt);
+        for (int t = 0; t < ndt; ++t) perm[t] = t;
+        std::stable_sort(perm.begin(), perm.end(), [&](int x, int y) { return tile_cost[x] > tile_cost[y]; });
+        std::vector<i32x4> tiles2((size_t)ndt);
+        std::vector<i32x2> tile_stages2((size_t)ndt);
+        std::vector<int32_t> base2(base.size());
+        std::vector<uint32_t> rec2(rec.size());
+        const size_t rec_block = (size_t)ngroups * W * D;
+        for (int i = 0; i < ndt; ++i) {
+            const int t = perm[i];
+            tiles2[i] = tiles[t];
+            tile_stages2[i] = tile_stages[t];
+            if (!base.empty())
+                std::copy_n(base.begin() + (size_t)t * nchan, nchan, base2.begin() + (size_t)i * nchan);
+            std::copy_n(rec.begin() + (size_t)t * rec_block, rec_block, rec2.begin() + (size_t)i * rec_block);
+        }
+        tiles.swap(tiles2);
+        tile_stages.swap(tile_stages2);
+        base.swap(base2);
+        rec.swap(rec2);
     }
     const int64_t lds_total = lds_cap;
     if (lds_total > 160 * 1024) {
@@ -2071,6 +2107,11 @@ void reset_tables(pu_plan *p)
 int finish_plan(pu_plan *p, const int64_t *shifts)
 {
     p->shifts.assign(shifts, shifts + p->ndm * p->nchan);
+    // subband item order: DM-tile major (longest items first) when a launch gives the
+    // CUs only a few items each, where the tail of unequal items weighs; time-tile major
+    // otherwise (L2 sharing across DM tiles).  PU_DT_MAJOR overrides (tuning).
+    p->dt_major = p->group > 1 && (int64_t)p->ndt * p->ntt < kDtMajorItems ? 1 : 0;
+    if (const char *env = getenv("PU_DT_MAJOR")) p->dt_major = atoi(env) != 0;
     return pu::hip_check(hipHostMalloc((void **)&p->h_cert, sizeof(CertState), hipHostMallocDefault),
                          "hipHostMalloc(cert)");
 }
