@@ -1216,7 +1216,10 @@ int pu_median(const double *x, int64_t n, double *out, void *ws, size_t ws_bytes
     uint32_t *hist = reinterpret_cast<uint32_t *>(st + 1);
     hipLaunchKernelGGL(median_init_kernel, dim3(1), dim3(256), 0, s, st, hist, n);
     // a few elements per thread: fewer workgroups to flush LDS bins to the global histogram
-    const unsigned grid = std::min<int64_t>(256, std::max<int64_t>(1, (n + 1023) / 1024));
+    // (PU_MEDIAN_GRID: most workgroups per pass, tuning)
+    int64_t gmax = 256;
+    if (const char *e = getenv("PU_MEDIAN_GRID")) gmax = std::max(1, atoi(e));
+    const unsigned grid = std::min<int64_t>(gmax, std::max<int64_t>(1, (n + 1023) / 1024));
     for (int p = 0; p < kMedPasses; ++p)
         hipLaunchKernelGGL(median_hist_kernel, dim3(grid), dim3(256), 0, s, x, n, st, hist, p);
     hipLaunchKernelGGL(median_final_kernel, dim3(1), dim3(256), 0, s, st, hist, n, out);

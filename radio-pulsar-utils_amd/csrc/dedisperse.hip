@@ -290,19 +290,7 @@ PU_MAX_DPP(max_qp1032, "quad_perm:[1,0,3,2] row_mask:0xf")
 PU_MAX_DPP(max_qp2301, "quad_perm:[2,3,0,1] row_mask:0xf")
 PU_MAX_DPP(max_ror4, "row_ror:4 row_mask:0xf")
 PU_MAX_DPP(max_ror8, "row_ror:8 row_mask:0xf")
-PU_MAX_DPP(max_bc15, "row_bcast:15 row_mask:0xa")
-PU_MAX_DPP(max_bc31, "row_bcast:31 row_mask:0xc")
 #undef PU_MAX_DPP
-
-__device__ __forceinline__ float wave_max_to63_dpp(float v)
-{
-    v = max_qp1032(v);
-    v = max_qp2301(v);
-    v = max_ror4(v);
-    v = max_ror8(v);
-    v = max_bc15(v);
-    return max_bc31(v);
-}
 
 __device__ __forceinline__ float vmax(float a, float b)
 {
@@ -313,18 +301,75 @@ __device__ __forceinline__ float vmax(float a, float b)
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// v_max3_f32 (IEEE mode: a NaN operand is skipped, as by v_max_f32)
+__device__ __forceinline__ float vmax3(float a, float b, float c)
+{
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// Cross-lane combines by the gfx950 permlane swaps (VALU, no LDS): one instruction
+// exchanges half of two registers, so one swap + one op reduces TWO values by a factor
+// of two in lanes.  swap32: lanes 0-31 of the result = op(a[l], a[l + 32]), lanes 32-63
+// = op(b[l - 32], b[l]).  swap16 (rows of 16 lanes): [op(a.r0, a.r1), op(b.r0, b.r1),
+// op(a.r2, a.r3), op(b.r2, b.r3)].
+template <class Op>
+__device__ __forceinline__ float swap32_combine(float a, float b, Op op)
+{
+    const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, a), __builtin_bit_cast(unsigned, b),
+                                                    false, false);
+    return op(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
+}
+template <class Op>
+__device__ __forceinline__ float swap16_combine(float a, float b, Op op)
+{
+    const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, a), __builtin_bit_cast(unsigned, b),
+                                                    false, false);
+    return op(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
+}
+
+// Row of 16 lanes: every lane gets the row's sum / max (fused DPP ops).
+__device__ __forceinline__ float row_allsum(float v)
+{
+    v += dpp_undef<0xB1>(v);
+    v += dpp_undef<0x4E>(v);
+    v += dpp_undef<0x124>(v);
+    v += dpp_undef<0x128>(v);
+    return v;
+}
+__device__ __forceinline__ float row_allmax(float v)
+{
+    v = max_qp1032(v);
+    v = max_qp2301(v);
+    v = max_ror4(v);
+    return max_ror8(v);
+}
+
 // Search-mode outputs of a wave of the subband kernel for a FULL time tile (every width's
 // windows inside the series): the statistics of write_outputs (same partial record) from
-// the packed accumulator pairs, without per-sample bounds tests.  Width 1 runs on the
-// pairs (v_pk_*); widths 2/4/8 on scalars (the 4- and 8-sample sums are single fused
-// v_add_f32_dpp row shifts - packing them would cost a DPP move per half) and count only
-// on lanes where they are aligned windows, by selects computed unconditionally (a
-// conditional v_max in inline asm became an EXEC-mask branch); maxima by v_max_f32 and the
-// wave reduction of maxima by v_max_f32_dpp.
+// the packed accumulator pairs, without per-sample bounds tests.
+//  * Per lane and trial: width 1 on the pairs (v_pk_*), widths 2/4/8 on scalars (the 4-
+//    and 8-sample sums are fused v_add_f32_dpp row shifts) counted only on lanes where
+//    they are aligned windows, by selects computed unconditionally (a conditional v_max in
+//    inline asm became an EXEC-mask branch); squares accumulated by FMA (one rounding),
+//    maxima by v_max3_f32 / v_max_f32.
+//  * Across the wave, 8 trials at once: permlane32 swaps pair trial k with k + 4 (half
+//    the lanes each), permlane16 swaps pair those with k + 2, so each of 2 registers
+//    holds 4 trials' partials in its 4 rows; 4 DPP steps finish every row.
+//    Per 8 trials and statistic: 6 swaps, 6 ops and 8 DPP steps instead of 6 DPP steps
+//    per trial (the previous epilogue: ~10 % of the kernel's wave cycles at C2).
+//  * Sums in float32 throughout: <= 14 float32 roundings per term (the shifted value, the
+//    4-term lane chain, the pair, 2 swaps, 4 row steps, the square), within the gamma =
+//    2^-20 the finalize kernel's certification assumes.
+//  * Stores: lane 16 r + i writes field i (< 13) of the record of row r's trial - one
+//    store instruction per 4 trials' records instead of one per field and trial.
 template <int D, int J>
 __device__ __forceinline__ void stats_full_pairs(const f32x2 (&acc)[D][J], const DedispArgs &a, int first, int slot0,
                                                  int cnt, int tt, int lane)
 {
+    static_assert(D % 8 == 0, "trials per wave");
+    constexpr int NV = 9;  // per trial: sum y, sum of squares w = 1,2,4,8, max w = 1,2,4,8
     const bool even = (lane & 1) == 0, quad = (lane & 3) == 0;
     // The shift (recorded as the partial's center): the tile mean of the wave's first
     // trial.  The wave's D trials are a few DM steps apart, so their tile means differ by
@@ -340,11 +385,9 @@ __device__ __forceinline__ void stats_full_pairs(const f32x2 (&acc)[D][J], const
         kt = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63)) *
              (1.0f / (128.0f * J));
     }
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-        if (slot0 + d >= cnt) continue;
-        const f32x2 k1 = {kt, kt};
-        const float k2 = 2.0f * kt, k4 = 4.0f * kt, k8 = 8.0f * kt;
+    const f32x2 k1 = {kt, kt};
+    const float k2 = 2.0f * kt, k4 = 4.0f * kt, k8 = 8.0f * kt;
+    auto lane_stats = [&](int d, float (&v)[NV]) {
         f32x2 s1 = {0.0f, 0.0f}, q1 = s1;
         float q2 = 0.0f, q4 = 0.0f, q8 = 0.0f;
         float m1 = -INFINITY, m2 = -INFINITY, m4 = -INFINITY, m8 = -INFINITY;
@@ -353,35 +396,71 @@ __device__ __forceinline__ void stats_full_pairs(const f32x2 (&acc)[D][J], const
             const f32x2 x = acc[d][j];
             const f32x2 y = x - k1;
             s1 += y;
-            q1 += y * y;
-            m1 = vmax(m1, vmax(x.x, x.y));
+            q1 = __builtin_elementwise_fma(y, y, q1);
+            m1 = vmax3(m1, x.x, x.y);
             const float r2 = x.x + x.y;                 // width 2 (every lane)
             const float y2 = r2 - k2;
-            q2 += y2 * y2;
+            q2 = __builtin_fmaf(y2, y2, q2);
             m2 = vmax(m2, r2);
             const float r4 = r2 + row_down<1>(r2);      // width 4 (even lanes)
             const float y4 = even ? r4 - k4 : 0.0f;
-            q4 += y4 * y4;
+            q4 = __builtin_fmaf(y4, y4, q4);
             m4 = vmax(m4, even ? r4 : -INFINITY);
             const float r8 = r4 + row_down<2>(r4);      // width 8 (lanes 4k)
             const float y8 = quad ? r8 - k8 : 0.0f;
-            q8 += y8 * y8;
+            q8 = __builtin_fmaf(y8, y8, q8);
             m8 = vmax(m8, quad ? r8 : -INFINITY);
         }
-        double *p = a.partials + ((size_t)(first + slot0 + d) * a.ntt + tt) * kPartStride;
-        const double x1 = wave_sum_to63_acc<float>(s1.x + s1.y);
-        const float mw[4] = {wave_max_to63_dpp(m1), wave_max_to63_dpp(m2), wave_max_to63_dpp(m4),
-                             wave_max_to63_dpp(m8)};
-        const double xq[4] = {wave_sum_to63_acc<float>(q1.x + q1.y), wave_sum_to63_acc<float>(q2),
-                              wave_sum_to63_acc<float>(q4), wave_sum_to63_acc<float>(q8)};
-        if (lane == 63) {
-            p[0] = static_cast<double>(kt);
+        v[0] = s1.x + s1.y;
+        v[1] = q1.x + q1.y;
+        v[2] = q2;
+        v[3] = q4;
+        v[4] = q8;
+        v[5] = m1;
+        v[6] = m2;
+        v[7] = m4;
+        v[8] = m8;
+    };
+    auto add = [](float x, float y) { return x + y; };
+    auto mx = [](float x, float y) { return vmax(x, y); };
+    // record field f = lane & 15 (< 13): kt | max w, sum, sum of squares w (w = 1, 2, 4, 8)
+    const int f = lane & 15, row = lane >> 4;
+    const int fw = (f - 1) / 3, fk = (f - 1) % 3;  // f >= 1: width index, 0 max / 1 sum / 2 squares
+    // 8 trials at a time (b0 .. b0 + 7): the register footprint of the 16-trial shapes'
+    // two passes is that of one
+#pragma unroll
+    for (int b0 = 0; b0 < D; b0 += 8) {
+        // trials k and k + 4 -> U[k] (lanes 0-31: k, 32-63: k + 4)
+        float U[4][NV];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float va[NV], vb[NV];
+            lane_stats(b0 + k, va);
+            lane_stats(b0 + k + 4, vb);
+#pragma unroll
+            for (int i = 0; i < NV; ++i)
+                U[k][i] = i < 5 ? swap32_combine(va[i], vb[i], add) : swap32_combine(va[i], vb[i], mx);
+        }
+        // U[j] and U[j + 2] -> W[j]: row r holds trial j + 2 r
+        float W[2][NV];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int i = 0; i < NV; ++i)
+                W[j][i] = i < 5 ? row_allsum(swap16_combine(U[j][i], U[j + 2][i], add))
+                                : row_allmax(swap16_combine(U[j][i], U[j + 2][i], mx));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            float v = kt;
 #pragma unroll
             for (int w = 0; w < 4; ++w) {
-                p[1 + 3 * w] = static_cast<double>(mw[w]);
-                p[2 + 3 * w] = x1;
-                p[3 + 3 * w] = xq[w];
+                v = (f >= 1 && fw == w && fk == 0) ? W[j][5 + w] : v;
+                v = (f >= 1 && fw == w && fk == 1) ? W[j][0] : v;
+                v = (f >= 1 && fw == w && fk == 2) ? W[j][1 + w] : v;
             }
+            const int trial = b0 + j + 2 * row;
+            if (f < 13 && slot0 + trial < cnt)
+                a.partials[((size_t)(first + slot0 + trial) * a.ntt + tt) * kPartStride + f] = static_cast<double>(v);
         }
     }
 }

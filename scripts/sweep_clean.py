@@ -2,7 +2,7 @@
 
 Times each C-ABI call with torch events (the calls run on torch's current stream)
 under every setting of the kernels' tuning variables (PU_CLEAN_VMAX, PU_CLEAN_BATCH,
-PU_CLEAN_SCALE_ROWS, PU_CLEAN_NT; read per call), plus renormalize_device end to end.
+PU_CLEAN_SCALE_ROWS, PU_CLEAN_NT, PU_MEDIAN_GRID; read per call), plus renormalize_device end to end.
 One JSON line per (dtype, kernel, setting).
 
     python scripts/sweep_clean.py [--dtype f32,u8] [--steps 20]
@@ -103,8 +103,13 @@ def main():
             rec("ceiling_f64_copy", {}, ms, 2 * nchan * n * 8)
             del y
         if "median" in want:
-            ms = timed(lambda: clean.median_device(lc), args.steps)
-            rec("median", {}, ms, n * 8)
+            # the real light curve (column means over good channels), not uninitialised memory
+            lib.pu_col_means(_hip.ptr(x), code, nchan, n, x.stride(0), _hip.ptr(bad), _hip.ptr(lc), s)
+            for g in (256, 128, 64, 32):
+                setenv(PU_MEDIAN_GRID=g)
+                ms = timed(lambda: clean.median_device(lc), args.steps)
+                rec("median", {"grid": g}, ms, n * 8)
+            setenv(PU_MEDIAN_GRID=None)
         for cut in ((False, True) if "renormalize_device" in want else ()):
             ms = timed(lambda: clean.renormalize_device(x, badchans_mask=bad_np, cut_outliers=cut, out=out),
                        args.steps)
