@@ -350,10 +350,10 @@ __device__ __forceinline__ float row_allmax(float v)
 // windows inside the series): the statistics of write_outputs (same partial record) from
 // the packed accumulator pairs, without per-sample bounds tests.
 //  * Per lane and trial: width 1 on the pairs (v_pk_*), widths 2/4/8 on scalars (the 4-
-//    and 8-sample sums are fused v_add_f32_dpp row shifts) counted only on lanes where
-//    they are aligned windows, by selects computed unconditionally (a conditional v_max in
-//    inline asm became an EXEC-mask branch); squares accumulated by FMA (one rounding),
-//    maxima by v_max3_f32 / v_max_f32.
+//    and 8-sample sums are fused v_add_f32_dpp row shifts) accumulated on every lane and
+//    kept only on lanes where they are aligned windows, by one select after the loop (a
+//    conditional v_max in inline asm became an EXEC-mask branch); squares accumulated by
+//    FMA (one rounding), maxima by v_max3_f32 / v_max_f32.
 //  * Across the wave, 8 trials at once: permlane32 swaps pair trial k with k + 4 (half
 //    the lanes each), permlane16 swaps pair those with k + 2, so each of 2 registers
 //    holds 4 trials' partials in its 4 rows; 4 DPP steps finish every row.
@@ -402,24 +402,26 @@ __device__ __forceinline__ void stats_full_pairs(const f32x2 (&acc)[D][J], const
             const float y2 = r2 - k2;
             q2 = __builtin_fmaf(y2, y2, q2);
             m2 = vmax(m2, r2);
-            const float r4 = r2 + row_down<1>(r2);      // width 4 (even lanes)
-            const float y4 = even ? r4 - k4 : 0.0f;
+            // widths 4 and 8 on every lane; only even lanes (4) / lanes 4k (8) hold aligned
+            // windows, so the others' sums and maxima are dropped once, after the loop
+            const float r4 = r2 + row_down<1>(r2);
+            const float y4 = r4 - k4;
             q4 = __builtin_fmaf(y4, y4, q4);
-            m4 = vmax(m4, even ? r4 : -INFINITY);
-            const float r8 = r4 + row_down<2>(r4);      // width 8 (lanes 4k)
-            const float y8 = quad ? r8 - k8 : 0.0f;
+            m4 = vmax(m4, r4);
+            const float r8 = r4 + row_down<2>(r4);
+            const float y8 = r8 - k8;
             q8 = __builtin_fmaf(y8, y8, q8);
-            m8 = vmax(m8, quad ? r8 : -INFINITY);
+            m8 = vmax(m8, r8);
         }
         v[0] = s1.x + s1.y;
         v[1] = q1.x + q1.y;
         v[2] = q2;
-        v[3] = q4;
-        v[4] = q8;
+        v[3] = even ? q4 : 0.0f;
+        v[4] = quad ? q8 : 0.0f;
         v[5] = m1;
         v[6] = m2;
-        v[7] = m4;
-        v[8] = m8;
+        v[7] = even ? m4 : -INFINITY;
+        v[8] = quad ? m8 : -INFINITY;
     };
     auto add = [](float x, float y) { return x + y; };
     auto mx = [](float x, float y) { return vmax(x, y); };
