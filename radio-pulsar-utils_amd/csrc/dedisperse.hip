@@ -2076,10 +2076,16 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
         }
         tile_cost[t] = (double)(lds_tile - lds_before) + 3.0e6 * tile_stages[t][1];
     }
-    // DM tiles in decreasing cost order (the kernel's DM-tile-major item order then
-    // dispatches the longest items first).  A tile's trials are named by its record, so
-    // the order changes nothing else.
-    {
+    // Item order: DM-tile major (longest items first) when the launch gives the CUs only
+    // a few items each, where the tail of unequal items weighs; time-tile major otherwise
+    // (the DM tiles of one time tile together on one XCD, sharing L2).  PU_DT_MAJOR
+    // overrides (tuning).  DM-tile major sorts the DM tiles by decreasing cost; a tile's
+    // trials are named by its record, so the order changes nothing else.  (Sorting them
+    // for the time-tile-major order too cost C3 1.1 % - 1109 vs 1122 ms.)
+    const int64_t ntt_plan = (n + TT - 1) / TT;
+    bool dt_major = (int64_t)ndt * ntt_plan < kDtMajorItems;
+    if (const char *env = getenv("PU_DT_MAJOR")) dt_major = atoi(env) != 0;
+    if (dt_major) {
         std::vector<int> perm((size_t)ndt);
         for (int t = 0; t < ndt; ++t) perm[t] = t;
         std::stable_sort(perm.begin(), perm.end(), [&](int x, int y) { return tile_cost[x] > tile_cost[y]; });
@@ -2130,6 +2136,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     p->lds_bytes = (size_t)lds_total;
     p->nslots_total = (int)(slotmeta.size() / ms);
     p->nstages = (int64_t)stages.size();
+    p->dt_major = dt_major ? 1 : 0;
     p->exec_adds = adds_tile * ntt;
     p->lds_traffic = lds_tile * ntt;
     // host tables only: the caller uploads the plan it keeps (upload_sub), so comparing
@@ -2188,11 +2195,6 @@ void reset_tables(pu_plan *p)
 int finish_plan(pu_plan *p, const int64_t *shifts)
 {
     p->shifts.assign(shifts, shifts + p->ndm * p->nchan);
-    // subband item order: DM-tile major (longest items first) when a launch gives the
-    // CUs only a few items each, where the tail of unequal items weighs; time-tile major
-    // otherwise (L2 sharing across DM tiles).  PU_DT_MAJOR overrides (tuning).
-    p->dt_major = p->group > 1 && (int64_t)p->ndt * p->ntt < kDtMajorItems ? 1 : 0;
-    if (const char *env = getenv("PU_DT_MAJOR")) p->dt_major = atoi(env) != 0;
     return pu::hip_check(hipHostMalloc((void **)&p->h_cert, sizeof(CertState), hipHostMallocDefault),
                          "hipHostMalloc(cert)");
 }
