@@ -2396,33 +2396,42 @@ int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int
         // tables are uploaded.  A candidate that does not fit (PU_EUNSUPPORTED) is not
         // viable; any other error is returned as is.
         auto cost = [](const pu_plan *q) { return (double)q->lds_traffic + 3.0e6 * (double)q->nstages * q->ntt; };
-        pu_plan *q = new pu_plan();
-        q->dtype = p->dtype;
-        q->acc = p->acc;
-        q->variant = p->variant;
-        q->nchan = p->nchan;
-        q->n = p->n;
-        q->ndm = p->ndm;
-        q->K = p->K;
-        q->TT = p->TT;
-        q->ntt = p->ntt;
+        auto fresh = [&]() {
+            pu_plan *q = new pu_plan();
+            q->dtype = p->dtype;
+            q->acc = p->acc;
+            q->variant = p->variant;
+            q->nchan = p->nchan;
+            q->n = p->n;
+            q->ndm = p->ndm;
+            q->K = p->K;
+            q->TT = p->TT;
+            q->ntt = p->ntt;
+            return q;
+        };
+        // Round 3: float32 inputs also weigh the tall shape (256 trials x 256 samples, G = 4):
+        // with the permlane epilogue it wins at C2 (14.91 vs 15.24 ms) and C5 (0.364 vs
+        // 0.383), loses at C4 (100 trials: 0.662 vs 0.581), and the same cost model ranks all
+        // three right.  8-bit inputs keep the wide shape (the byte-count model undercounts
+        // their u8 slot-build reads: tall G = 4 at C3 625 trials 135.8 vs wide G = 8 132.1).
+        const bool try_tall = dtype == PU_F32 && !getenv("PU_SUB_SHAPE");
+        pu_plan *q = fresh(), *t = try_tall ? fresh() : nullptr;
         const int rc8 = plan_sub(q, shifts, 8, shape, sub_budget);
         const int rc4 = plan_sub(p, shifts, 4, shape, sub_budget);
-        for (int r : {rc8, rc4}) {
+        const int rct = t ? plan_sub(t, shifts, 4, SUB_TALL, 160 * 1024) : PU_EUNSUPPORTED;
+        for (int r : {rc8, rc4, rct}) {
             if (r != PU_OK && r != PU_EUNSUPPORTED) {
                 free_plan(q);
                 free_plan(p);
+                free_plan(t);
                 return r;
             }
         }
         pu_plan *keep = nullptr;
-        if (rc8 == PU_OK && (rc4 != PU_OK || cost(p) > cost(q))) {
-            free_plan(p);
-            keep = q;
-        } else if (rc4 == PU_OK) {
-            free_plan(q);
-            keep = p;
-        }
+        for (auto [cand, ok] : {std::pair<pu_plan *, bool>{p, rc4 == PU_OK}, {q, rc8 == PU_OK}, {t, rct == PU_OK}})
+            if (ok && (!keep || cost(cand) < cost(keep))) keep = cand;
+        for (pu_plan *cand : {p, q, t})  // losers (p stays when nothing fits: it is reused below)
+            if (cand != keep && (keep || cand != p)) free_plan(cand);
         if (keep) {
             rc = upload_sub(keep);
             if (!rc) rc = finish_plan(keep, shifts);
@@ -2433,7 +2442,6 @@ int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int
             *out = keep;
             return PU_OK;
         }
-        free_plan(q);
         reset_tables(p);
         G = 2;  // 8 and 4 do not fit: continue with the smaller groups
     }

@@ -39,7 +39,7 @@ for v in variants:
             os.environ.pop(k, None)
         else:
             os.environ[k] = val
-    print("variant", v, json.dumps({k: plans[v].info[k] for k in ("group", "stages", "dm_tiles", "lds_bytes",
+    print("variant", v, json.dumps({k: plans[v].info[k] for k in ("group", "stages", "dm_tiles", "time_tiles", "lds_traffic", "lds_bytes",
                                                                     "slot_bytes", "raw_stride")}), flush=True)
 ws = torch.empty(max(p.workspace_bytes for p in plans.values()), dtype=torch.uint8, device=x.device)
 res = {v: [] for v in plans}

@@ -94,6 +94,8 @@ def main():
                     rec("apply", {"vmax": vmax, "nt": nt, "batch": batch}, ms, plane + nchan * n * 8)
         setenv(PU_CLEAN_VMAX=None, PU_CLEAN_NT=None, PU_APPLY_BATCH=None)
         if "ceiling" in want:
+            spec_f = torch.empty(nchan, dtype=torch.float32 if code == _hip.PU_F32 else torch.float64, device=x.device)
+            ws_rs = torch.empty(max(16, lib.pu_row_sums_workspace_bytes(nchan, n)), dtype=torch.uint8, device=x.device)
             # the same traffic (read the plane, write it as float64) by torch's own
             # elementwise cast kernel: the achievable rate for this read/write mix
             ms = timed(lambda: out.copy_(x), args.steps)
@@ -102,6 +104,12 @@ def main():
             ms = timed(lambda: y.copy_(out), args.steps)
             rec("ceiling_f64_copy", {}, ms, 2 * nchan * n * 8)
             del y
+            # write-only and read-only streams of the same plane sizes
+            ms = timed(lambda: out.fill_(1.0), args.steps)
+            rec("ceiling_f64_fill", {}, ms, nchan * n * 8)
+            ms = timed(lambda: lib.pu_row_sums(_hip.ptr(x), code, nchan, n, x.stride(0), 0, None, None, float(n),
+                                               _hip.ptr(spec_f), _hip.ptr(ws_rs), ws_rs.numel(), s), args.steps)
+            rec("ceiling_read_rowsum", {}, ms, plane)
         if "median" in want:
             # the real light curve (column means over good channels), not uninitialised memory
             lib.pu_col_means(_hip.ptr(x), code, nchan, n, x.stride(0), _hip.ptr(bad), _hip.ptr(lc), s)

@@ -348,12 +348,14 @@ def sampled_trials(snr, n):
     return np.unique(np.r_[np.linspace(0, snr.size - 1, n - 5).astype(int), top])
 
 
-@pytest.mark.parametrize("name,group", [("C2", 4), ("C3", 8), ("C5", 4)])
-def test_default_group_cost_model(gpu, golden, name, group):
-    """With no explicit group the planner keeps the cheaper of G = 8 / G = 4 by its cost
-    model; at C2/C3/C5 that is the measured winner (profiles/r01_autog/).  The default
-    plan's dedispersed rows also match the oracle (float32: the summation-order bound;
-    uint8: bit-exact), so the numerics do not depend on which G the model picks."""
+@pytest.mark.parametrize("name,group,tile", [("C2", 4, 256), ("C3", 8, 128), ("C5", 4, 256), ("C4", 4, 128)])
+def test_default_group_cost_model(gpu, golden, name, group, tile):
+    """With no explicit group the planner keeps the cheapest of G = 8 / G = 4 (wide shape,
+    128-trial DM tiles) and, for float32 input, the tall shape (256-trial tiles, G = 4) by
+    its cost model; at C2/C3/C4/C5 that is the measured winner (profiles/r01_autog/,
+    profiles/r03/experiments/ab_*_shape*.log).  The default plan's dedispersed rows also
+    match the oracle (float32: the summation-order bound; uint8: bit-exact), so the
+    numerics do not depend on which plan the model picks."""
     import torch
     from pulsarutils import synth
     c = CONFIGS[name]
@@ -361,7 +363,7 @@ def test_default_group_cost_model(gpu, golden, name, group):
     sh = _hip.shift_table(c.nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
     code = {"u8": _hip.PU_U8, "f32": _hip.PU_F32}[c.dtype]
     plan = _hip.Plan(code, _hip.PU_ACC_NATIVE, c.nchan, c.nsamples, sh)
-    assert plan.info["group"] == group, plan.info
+    assert plan.info["group"] == group and plan.info["trials_per_tile"] == tile, plan.info
     if name == "C3":
         return  # C3's default-plan rows are checked bit-exact in test_search_c3_full_size_u8
     xd = synth.pulsar_filterbank_device(c)
