@@ -2409,28 +2409,28 @@ int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int
             q->ntt = p->ntt;
             return q;
         };
-        // Round 3: float32 inputs also weigh the tall shape (256 trials x 256 samples, G = 4):
-        // with the permlane epilogue it wins at C2 (14.91 vs 15.24 ms) and C5 (0.364 vs
-        // 0.383), loses at C4 (100 trials: 0.662 vs 0.581), and the same cost model ranks all
-        // three right.  8-bit inputs keep the wide shape (the byte-count model undercounts
-        // their u8 slot-build reads: tall G = 4 at C3 625 trials 135.8 vs wide G = 8 132.1).
-        const bool try_tall = dtype == PU_F32 && !getenv("PU_SUB_SHAPE");
-        pu_plan *q = fresh(), *t = try_tall ? fresh() : nullptr;
+        // Round 3: the tall shape (256 trials x 256 samples) competes too, with G = 4 and 8.
+        // With the permlane epilogue the same cost model ranks every measured case right:
+        // C2 tall G4 14.92 ms (wide G4 15.23, tall G8 20.19), C3 tall G8 1042 ms (wide G8
+        // 1114; 625 trials 125.6 vs 132.4, tall G4 135.8), C5 tall G4 0.365 (wide 0.374),
+        // C4 wide G4 0.581 (100 trials: tall 0.662).  PU_SUB_SHAPE pins the shape.
+        const bool try_tall = !getenv("PU_SUB_SHAPE");
+        pu_plan *q = fresh(), *t4 = try_tall ? fresh() : nullptr, *t8 = try_tall ? fresh() : nullptr;
         const int rc8 = plan_sub(q, shifts, 8, shape, sub_budget);
         const int rc4 = plan_sub(p, shifts, 4, shape, sub_budget);
-        const int rct = t ? plan_sub(t, shifts, 4, SUB_TALL, 160 * 1024) : PU_EUNSUPPORTED;
-        for (int r : {rc8, rc4, rct}) {
+        const int rct4 = t4 ? plan_sub(t4, shifts, 4, SUB_TALL, 160 * 1024) : PU_EUNSUPPORTED;
+        const int rct8 = t8 ? plan_sub(t8, shifts, 8, SUB_TALL, 160 * 1024) : PU_EUNSUPPORTED;
+        for (int r : {rc8, rc4, rct4, rct8}) {
             if (r != PU_OK && r != PU_EUNSUPPORTED) {
-                free_plan(q);
-                free_plan(p);
-                free_plan(t);
+                for (pu_plan *c : {p, q, t4, t8}) free_plan(c);
                 return r;
             }
         }
         pu_plan *keep = nullptr;
-        for (auto [cand, ok] : {std::pair<pu_plan *, bool>{p, rc4 == PU_OK}, {q, rc8 == PU_OK}, {t, rct == PU_OK}})
+        for (auto [cand, ok] : {std::pair<pu_plan *, bool>{p, rc4 == PU_OK}, {q, rc8 == PU_OK}, {t4, rct4 == PU_OK},
+                                {t8, rct8 == PU_OK}})
             if (ok && (!keep || cost(cand) < cost(keep))) keep = cand;
-        for (pu_plan *cand : {p, q, t})  // losers (p stays when nothing fits: it is reused below)
+        for (pu_plan *cand : {p, q, t4, t8})  // losers (p stays when nothing fits: it is reused below)
             if (cand != keep && (keep || cand != p)) free_plan(cand);
         if (keep) {
             rc = upload_sub(keep);

@@ -348,11 +348,10 @@ def sampled_trials(snr, n):
     return np.unique(np.r_[np.linspace(0, snr.size - 1, n - 5).astype(int), top])
 
 
-@pytest.mark.parametrize("name,group,tile", [("C2", 4, 256), ("C3", 8, 128), ("C5", 4, 256), ("C4", 4, 128)])
+@pytest.mark.parametrize("name,group,tile", [("C2", 4, 256), ("C3", 8, 256), ("C5", 4, 256), ("C4", 4, 128)])
 def test_default_group_cost_model(gpu, golden, name, group, tile):
-    """With no explicit group the planner keeps the cheapest of G = 8 / G = 4 (wide shape,
-    128-trial DM tiles) and, for float32 input, the tall shape (256-trial tiles, G = 4) by
-    its cost model; at C2/C3/C4/C5 that is the measured winner (profiles/r01_autog/,
+    """With no explicit group the planner keeps the cheapest of G = 8 / G = 4 in the wide
+    (128-trial DM tiles) and tall (256-trial) shapes by its cost model; at C2/C3/C4/C5 that is the measured winner (profiles/r01_autog/,
     profiles/r03/experiments/ab_*_shape*.log).  The default plan's dedispersed rows also
     match the oracle (float32: the summation-order bound; uint8: bit-exact), so the
     numerics do not depend on which plan the model picks."""
