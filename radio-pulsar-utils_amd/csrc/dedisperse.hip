@@ -47,7 +47,8 @@ constexpr int kWaves = 8;                 // waves per workgroup (each owns D tr
 constexpr int kThreads = kWaves * 64;
 constexpr int kD = 8;                     // trials per wave
 constexpr int kTPT = kWaves * kD;         // trials per tile
-constexpr int kPartStride = 16;           // doubles per (trial, time tile) partial record
+constexpr int kPartStride = 16;           // elements per (trial, time tile) partial record: the
+                                          // accumulation type's (float: 64 B, double: 128 B)
 constexpr size_t kLdsBudget = 64 * 1024;  // per workgroup: 2 workgroups / CU
 constexpr int kMaxSpread = 2048;
 
@@ -66,7 +67,7 @@ struct DedispArgs {
     int32_t pad1;
     void *plane;
     int64_t ld_plane;
-    double *partials;
+    void *partials;  // float records for float32 accumulation, double for float64
 };
 
 // Uniform (scalar-cache) load: the constant address space makes hipcc emit s_load.
@@ -462,7 +463,7 @@ __device__ __forceinline__ void stats_full_pairs(const f32x2 (&acc)[D][J], const
             }
             const int trial = b0 + j + 2 * row;
             if (f < 13 && slot0 + trial < cnt)
-                a.partials[((size_t)(first + slot0 + trial) * a.ntt + tt) * kPartStride + f] = static_cast<double>(v);
+                reinterpret_cast<float *>(a.partials)[((size_t)(first + slot0 + trial) * a.ntt + tt) * kPartStride + f] = v;
         }
     }
 }
@@ -549,7 +550,7 @@ __device__ __forceinline__ void write_outputs(const Ta (&acc)[D][K], const Dedis
                     account(3, r, t, (lane & 7) == 0);
                 }
             }
-            double* p = a.partials + ((size_t)(first + slot0 + d) * a.ntt + tt) * kPartStride;
+            Ta *p = reinterpret_cast<Ta *>(a.partials) + ((size_t)(first + slot0 + d) * a.ntt + tt) * kPartStride;
             const bool full = t0 + J * 64 * E <= n;  // uniform
             double x1_0 = 0.0;
 #pragma unroll
@@ -562,12 +563,12 @@ __device__ __forceinline__ void write_outputs(const Ta (&acc)[D][K], const Dedis
                 if (w == 0) x1_0 = x1;
                 const double x2 = wave_sum_to63_acc<Ta>(s2[w]);
                 if (lane == 63) {
-                    p[1 + 3 * w] = static_cast<double>(m);
-                    p[2 + 3 * w] = x1;
-                    p[3 + 3 * w] = x2;
+                    p[1 + 3 * w] = m;
+                    p[2 + 3 * w] = static_cast<Ta>(x1);
+                    p[3 + 3 * w] = static_cast<Ta>(x2);
                 }
             }
-            if (lane == 63) p[0] = static_cast<double>(kt);
+            if (lane == 63) p[0] = kt;
         }
     }
 }
@@ -1320,20 +1321,21 @@ struct CertModel {
 // max - w mean is within its bound of 0 (the S/N sign decision), and - for plans whose
 // series is exact - when two S/N values of the strict first-best chain are within the
 // sum of their bounds (ties).
+template <typename PT>
 __global__ void __launch_bounds__(256)
-pu_finalize_kernel(const double *__restrict__ part, int ntt, int n, int tt_len,
+pu_finalize_kernel(const PT *__restrict__ part, int ntt, int n, int tt_len,
                    double *max_out, double *std_out, double *snr_out, int32_t *win_out,
                    CertModel cm, CertState *cert, int32_t *list)
 {
     __shared__ double red[4][4][256];
     const int trial = blockIdx.x;
     const int tid = threadIdx.x;
-    const double *p = part + (size_t)trial * ntt * kPartStride;
+    const PT *p = part + (size_t)trial * ntt * kPartStride;
     const double mu = p[0];
     double S1[4] = {0, 0, 0, 0}, S2[4] = {0, 0, 0, 0}, MX[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
     double A2[4] = {0, 0, 0, 0};
     for (int i = tid; i < ntt; i += 256) {
-        const double *q = p + (size_t)i * kPartStride;
+        const PT *q = p + (size_t)i * kPartStride;
         const double dk = q[0] - mu;
         for (int w = 0; w < 4; ++w) {
             const int width = 1 << w;
@@ -2199,7 +2201,10 @@ int finish_plan(pu_plan *p, const int64_t *shifts)
                          "hipHostMalloc(cert)");
 }
 
-size_t part_bytes(const pu_plan *p) { return ((size_t)p->ndm * p->ntt * kPartStride * sizeof(double) + 255) & ~size_t(255); }
+// partial records in the plan's accumulation type (the epilogues' sums are float32
+// for float32 accumulation: a float record stores them exactly)
+size_t part_elem(const pu_plan *p) { return kVariants[p->variant].acc_f64 ? sizeof(double) : sizeof(float); }
+size_t part_bytes(const pu_plan *p) { return ((size_t)p->ndm * p->ntt * kPartStride * part_elem(p) + 255) & ~size_t(255); }
 
 // Rounding model of the plan's fast statistics (pu_finalize_kernel).
 CertModel cert_model(const pu_plan *p)
@@ -2211,9 +2216,9 @@ CertModel cert_model(const pu_plan *p)
         m.gamma = 0x1p-44;
     } else if (p->dtype == PU_U8 && 8 * 255 * p->nchan < (int64_t(1) << 24)) {
         // integer sums (and their 8-sample rebins) below 2^24: exact in float32.  The
-        // epilogue's sums of squares: <= 12 float32 roundings of nonnegative terms (the
-        // square, 4 lane-local adds, the pair add, 4 row-reduction adds, the shifted
-        // value itself twice) = 12 x 2^-24 < 2^-20
+        // epilogue's sums of squares: <= 14 float32 roundings of nonnegative terms (the
+        // shifted value, the square-and-add, 4 lane-local adds, the pair add, 2 permlane
+        // and 4 row-reduction adds, the float record) = 14 x 2^-24 < 2^-20
         m.tie_check = 1;
         m.e_rel = 0.0;
         m.gamma = 0x1p-20;
@@ -2228,14 +2233,20 @@ CertModel cert_model(const pu_plan *p)
     return m;
 }
 
-int launch_finalize(pu_plan *p, const double *part, double *mx, double *sd, double *snr, int32_t *win, char *ws,
+int launch_finalize(pu_plan *p, const void *part, double *mx, double *sd, double *snr, int32_t *win, char *ws,
                     hipStream_t s)
 {
     CertState *cert = reinterpret_cast<CertState *>(ws + part_bytes(p));
     int32_t *list = reinterpret_cast<int32_t *>(cert + 1);
     PU_TRY_HIP(hipMemsetAsync(cert, 0, sizeof(CertState), s));
-    hipLaunchKernelGGL(pu_finalize_kernel, dim3((unsigned)p->ndm), dim3(256), 0, s, part, p->ntt, (int)p->n, p->TT,
-                       mx, sd, snr, win, cert_model(p), cert, list);
+    if (part_elem(p) == sizeof(float))
+        hipLaunchKernelGGL(pu_finalize_kernel<float>, dim3((unsigned)p->ndm), dim3(256), 0, s,
+                           reinterpret_cast<const float *>(part), p->ntt, (int)p->n, p->TT, mx, sd, snr, win, cert_model(p),
+                           cert, list);
+    else
+        hipLaunchKernelGGL(pu_finalize_kernel<double>, dim3((unsigned)p->ndm), dim3(256), 0, s,
+                           reinterpret_cast<const double *>(part), p->ntt, (int)p->n, p->TT, mx, sd, snr, win, cert_model(p),
+                           cert, list);
     return pu::launch_check("pu_finalize_kernel");
 }
 
@@ -2571,7 +2582,7 @@ int pu_plan_search_tiles(pu_plan *p, const void *data, int64_t ld, int64_t tt_be
     PU_REQUIRE(workspace && ws_bytes >= pu_plan_workspace_bytes(p), "pu_plan_search_tiles: workspace too small");
     if (tt_begin == tt_end) return PU_OK;
     DedispArgs a = make_args(p, data, ld);
-    a.partials = reinterpret_cast<double *>(workspace);
+    a.partials = workspace;
     a.tt0 = (int32_t)tt_begin;
     a.ntt_run = (int32_t)(tt_end - tt_begin);
     return dispatch(p, a, false, pu::as_stream(stream));
@@ -2587,7 +2598,7 @@ int pu_plan_finalize(pu_plan *p, const void *data, int64_t ld, double *max_out, 
                "pu_plan_finalize: workspace too small or not 8-byte aligned");
     hipStream_t s = pu::as_stream(stream);
     char *ws = reinterpret_cast<char *>(workspace);
-    rc = launch_finalize(p, reinterpret_cast<const double *>(ws), max_out, std_out, snr_out, rebin_out, ws, s);
+    rc = launch_finalize(p, ws, max_out, std_out, snr_out, rebin_out, ws, s);
     if (rc) return rc;
     return resolve_flagged(p, data, ld, max_out, std_out, snr_out, rebin_out, ws, s);
 }
@@ -2601,7 +2612,7 @@ int pu_plan_search(pu_plan *p, const void *data, int64_t ld, double *max_out, do
     PU_REQUIRE(workspace && ws_bytes >= pu_plan_workspace_bytes(p) && reinterpret_cast<uintptr_t>(workspace) % 8 == 0,
                "pu_plan_search: workspace too small or not 8-byte aligned");
     DedispArgs a = make_args(p, data, ld);
-    a.partials = reinterpret_cast<double *>(workspace);
+    a.partials = workspace;
     hipStream_t s = pu::as_stream(stream);
     rc = dispatch(p, a, false, s);
     if (rc) return rc;
