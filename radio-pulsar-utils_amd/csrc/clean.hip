@@ -1013,12 +1013,15 @@ int col_means_t(const void *x, int64_t nrows, int64_t n, int64_t ld, const uint8
         }
     }
     const int v = pick_vec<Tin>(x, ld, vec_max(sizeof(Tin), 4));
-    // bytes of rows in flight per lane and register buffer (PU_CLEAN_BATCH: 128 or 256)
+    // bytes of rows in flight per lane and register buffer (PU_CLEAN_BATCH: 128, 256 or 512)
     int bb = 256;  // C4 sweep (profiles/r02_clean/): f32 V=4 190 us vs 212 us at 128 B
     if (const char *e = getenv("PU_CLEAN_BATCH")) bb = atoi(e);
     return column_launches<Tin>(v, n, [&](auto vc, int64_t col0, int64_t ncols) {
         constexpr int V = decltype(vc)::value;
-        if (bb >= 256)
+        if (bb >= 512)
+            hipLaunchKernelGGL((colmean_kernel<Tin, V, 512>), dim3(blocks_for(ncols / V, 256)), dim3(256), 0, s,
+                               reinterpret_cast<const Tin *>(x), nrows, col0, ncols, ld, skip, out);
+        else if (bb >= 256)
             hipLaunchKernelGGL((colmean_kernel<Tin, V, 256>), dim3(blocks_for(ncols / V, 256)), dim3(256), 0, s,
                                reinterpret_cast<const Tin *>(x), nrows, col0, ncols, ld, skip, out);
         else

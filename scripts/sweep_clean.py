@@ -73,7 +73,7 @@ def main():
                   flush=True)
 
         for vmax in ((1, 2, 4) if "col_means" in want else ()):
-            for batch in (128, 256):
+            for batch in (128, 256, 512):
                 setenv(PU_CLEAN_VMAX=vmax, PU_CLEAN_BATCH=batch)
                 ms = timed(lambda: lib.pu_col_means(_hip.ptr(x), code, nchan, n, x.stride(0), _hip.ptr(bad),
                                                     _hip.ptr(lc), s), args.steps)
