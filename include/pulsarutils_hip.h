@@ -206,6 +206,14 @@ int pu_ratio(double numerator, const double *x, int64_t n, double *out, void *st
  * out[0] on the device, bit-exact: radix select of the two middle order statistics,
  * numpy's mean of them; NaN if any element is NaN.  ws: pu_median_workspace_bytes(),
  * 8-byte aligned. */
+/* get_noisier_channels' decision (pulsarutils/clean.py:58-67 with stats.py:11-32 ref_mad):
+ * mask[i] = spec[i] > medfilt(spec, 7)[i] + 5 * ref_mad(spec), numpy's dtypes and order
+ * (spec float32 for float32 input, float64 otherwise; mad_c = statsmodels' MAD constant
+ * norm.ppf(3/4)).  One workgroup, 2 <= n <= 4096.  *flag = 1 (mask not written) when spec
+ * holds a NaN / inf: the caller decides those on the host. */
+int pu_noisy_channels(const void *spec, int dtype, int64_t n, double mad_c, uint8_t *mask, int32_t *flag,
+                      void *stream);
+
 size_t pu_median_workspace_bytes(void);
 int pu_median(const double *x, int64_t n, double *out, void *ws, size_t ws_bytes, void *stream);
 

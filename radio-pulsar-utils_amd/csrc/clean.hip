@@ -879,6 +879,104 @@ __global__ void __launch_bounds__(256) median_final_kernel(MedState *st, const u
     }
 }
 
+// ---------------------------------------------------------------- noisy channels
+// get_noisier_channels' decision on the device (clean.py:58-67, stats.py:11-32): one
+// workgroup, spec of n <= kNoisyMax channel means in T (float32 for float32 input, else
+// float64: numpy's mean dtype).  The host path it replaces did medfilt + ref_mad in numpy
+// after a read-back of spec; every step here keeps numpy's dtypes (NEP 50) and order:
+//   smooth = medfilt(spec, 7)           rank 3 of the zero-padded 7-window (T, exact)
+//   d = diff(spec)                      T
+//   m = median(d)                       T: the middle element, or (a + b) / 2 in T
+//   e = |d - m| / c                     |.| in T, then / c (numpy float64 scalar) in float64
+//   rm = median(e) / sqrt(2)            float64
+//   mask = spec > smooth + 5 rm         float64
+// A non-finite spec (NaN / inf: medfilt's and median's handling of them is left to
+// numpy / scipy) sets *flag and leaves mask unwritten: the caller then takes the host path.
+constexpr int kNoisyMax = 4096;
+
+template <typename T>
+__device__ void bitonic_sort_lds(T *v, int m)  // m: power of two, 1024 threads
+{
+    for (int k = 2; k <= m; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < m; i += 1024) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const T a = v[i], b = v[l];
+                    const bool up = (i & k) == 0;
+                    if (up ? (b < a) : (a < b)) {
+                        v[i] = b;
+                        v[l] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+}
+
+template <typename T>
+__device__ T median_sorted(const T *v, int cnt)  // numpy: middle element / mean of the two
+{
+    if (cnt & 1) return v[cnt / 2];
+    const T s = v[cnt / 2 - 1] + v[cnt / 2];
+    return s / T(2);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(1024)
+noisy_channels_kernel(const T *__restrict__ spec, int n, double c, uint8_t *__restrict__ mask,
+                      int32_t *__restrict__ flag)
+{
+    __shared__ T sp[kNoisyMax];
+    __shared__ double buf[kNoisyMax];  // the sorted differences (T), then the sorted e (float64)
+    T *dv = reinterpret_cast<T *>(buf);
+    double *ev = buf;
+    const int tid = threadIdx.x;
+    int nonfinite = 0;
+    for (int i = tid; i < n; i += 1024) {
+        const T v = spec[i];
+        sp[i] = v;
+        nonfinite |= !isfinite((double)v);
+    }
+    if (__syncthreads_or(nonfinite)) {
+        if (tid == 0) flag[0] = 1;
+        return;
+    }
+    int m = 1;
+    while (m < n - 1) m <<= 1;
+    for (int i = tid; i < m; i += 1024) dv[i] = i < n - 1 ? T(sp[i + 1] - sp[i]) : T(INFINITY);
+    __syncthreads();
+    bitonic_sort_lds(dv, m);
+    const T med = median_sorted(dv, n - 1);
+    __syncthreads();  // every thread has read the median before buf is overwritten
+    for (int i = tid; i < m; i += 1024)
+        ev[i] = i < n - 1 ? (double)T(fabs(T(sp[i + 1] - sp[i]) - med)) / c : INFINITY;
+    __syncthreads();
+    bitonic_sort_lds(ev, m);
+    const double rm = median_sorted(ev, n - 1) / 1.4142135623730951;  // np.sqrt(2)
+    const double thr = 5.0 * rm;
+    for (int i = tid; i < n; i += 1024) {
+        T w[7];
+#pragma unroll
+        for (int j = 0; j < 7; ++j) {
+            const int k = i + j - 3;
+            w[j] = (k >= 0 && k < n) ? sp[k] : T(0);
+        }
+        // rank 3 of 7 (a full insertion sort of the window: exact selection)
+#pragma unroll
+        for (int a = 1; a < 7; ++a)
+#pragma unroll
+            for (int b = a; b > 0; --b)
+                if (w[b] < w[b - 1]) {
+                    const T t = w[b];
+                    w[b] = w[b - 1];
+                    w[b - 1] = t;
+                }
+        mask[i] = (double)sp[i] > (double)w[3] + thr ? 1 : 0;
+    }
+    if (tid == 0) flag[0] = 0;
+}
+
 __global__ void ratio_dev_kernel(const double *__restrict__ num, const double *__restrict__ x, int64_t n,
                                  double *__restrict__ out)
 {
@@ -1227,6 +1325,21 @@ int pu_median(const double *x, int64_t n, double *out, void *ws, size_t ws_bytes
         hipLaunchKernelGGL(median_hist_kernel, dim3(grid), dim3(256), 0, s, x, n, st, hist, p);
     hipLaunchKernelGGL(median_final_kernel, dim3(1), dim3(256), 0, s, st, hist, n, out);
     return pu::launch_check("median_kernels");
+}
+
+int pu_noisy_channels(const void *spec, int dtype, int64_t n, double mad_c, uint8_t *mask, int32_t *flag,
+                      void *stream)
+{
+    PU_REQUIRE(spec && mask && flag, "pu_noisy_channels: NULL pointer");
+    PU_REQUIRE(n >= 2 && n <= kNoisyMax, "pu_noisy_channels: n = %lld outside [2, %d]", (long long)n, kNoisyMax);
+    PU_REQUIRE(dtype == PU_F32 || dtype == PU_F64, "pu_noisy_channels: spec must be float32 or float64");
+    if (dtype == PU_F32)
+        hipLaunchKernelGGL(noisy_channels_kernel<float>, dim3(1), dim3(1024), 0, pu::as_stream(stream),
+                           reinterpret_cast<const float *>(spec), (int)n, mad_c, mask, flag);
+    else
+        hipLaunchKernelGGL(noisy_channels_kernel<double>, dim3(1), dim3(1024), 0, pu::as_stream(stream),
+                           reinterpret_cast<const double *>(spec), (int)n, mad_c, mask, flag);
+    return pu::launch_check("noisy_channels_kernel");
 }
 
 int pu_ratio_dev(const double *numerator, const double *x, int64_t n, double *out, void *stream)

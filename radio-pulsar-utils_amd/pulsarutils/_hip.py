@@ -48,6 +48,7 @@ SIGNATURES = {
     "pu_ratio": (_i32, [_f64, _vp, _i64, _vp, _vp]),
     "pu_median_workspace_bytes": (_sz, []),
     "pu_median": (_i32, [_vp, _i64, _vp, _vp, _sz, _vp]),
+    "pu_noisy_channels": (_i32, [_vp, _i32, _i64, _f64, _vp, _vp, _vp]),
     "pu_ratio_dev": (_i32, [_vp, _vp, _i64, _vp, _vp]),
     "pu_renorm_apply": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
     "pu_renorm_apply_zero_dm": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp]),

@@ -20,7 +20,7 @@ from . import _hip
 from .dedispersion import (dedispersion_plan, dedispersion_shifts,  # noqa: F401
                            apply_dm_shifts_to_data, quick_resample, quick_chan_rebin)
 from .dedispersion import dedispersion_search as fast_dedispersion_search  # noqa: F401
-from .stats import mad, ref_mad
+from .stats import MAD_C, mad, ref_mad
 from .table import make_table
 
 
@@ -122,10 +122,29 @@ def _host(t):
     return t.detach().cpu().numpy()
 
 
+_NOISY_MAX = 4096  # pu_noisy_channels: one workgroup
+
+
 def get_noisier_channels(array):
-    """clean.py:58-67: channels whose mean exceeds medfilt(spec, 7) + 5 ref_mad."""
+    """clean.py:58-67: channels whose mean exceeds medfilt(spec, 7) + 5 ref_mad.
+
+    The decision runs on the device (pu_noisy_channels: medfilt, ref_mad and the
+    comparison in numpy's dtypes and order) and only the mask comes back; a spec with
+    NaN / inf, or more than 4096 channels, is decided on the host by numpy / scipy."""
     x = _hip.to_device(array)
-    spec = _host(channel_means_device(x))
+    spec_d = channel_means_device(x)
+    n = spec_d.numel()
+    if 2 <= n <= _NOISY_MAX:
+        t = _hip.torch()
+        off = (n + 3) & ~3
+        res = t.empty(off + 4, dtype=t.uint8, device=spec_d.device)  # mask, then the int32 flag
+        _hip.check(_hip.lib().pu_noisy_channels(_hip.ptr(spec_d), _hip.dtype_code(spec_d.dtype), n, float(MAD_C),
+                                                _hip.ptr(res), res.data_ptr() + off, _hip.stream_ptr()),
+                   "pu_noisy_channels")
+        h = _host(res)
+        if not h[off:off + 4].view(np.int32)[0]:
+            return h[:n].astype(bool)
+    spec = _host(spec_d)
     smooth_spec = medfilt(spec, 7)
     return spec > smooth_spec + 5 * ref_mad(spec)
 

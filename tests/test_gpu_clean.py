@@ -233,3 +233,64 @@ def test_col_means_u8_segments(gpu, nrows, ncols):
     with np.errstate(invalid="ignore"):
         ref = x[good].astype(np.float64).sum(axis=0) / float(good.sum())
     np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+def _noisy_host(spec):
+    """The reference's decision (clean.py:58-67) on a host spec, numpy / scipy."""
+    from scipy.signal import medfilt
+    from pulsarutils.stats import ref_mad
+    return spec > medfilt(spec, 7) + 5 * ref_mad(spec)
+
+
+def _noisy_device(spec):
+    import torch
+    from pulsarutils import _hip
+    d = torch.from_numpy(spec).cuda()
+    n = spec.size
+    off = (n + 3) & ~3
+    res = torch.full((off + 4,), 7, dtype=torch.uint8, device=d.device)
+    _hip.check(_hip.lib().pu_noisy_channels(_hip.ptr(d), _hip.dtype_code(d.dtype), n, float(C.MAD_C), _hip.ptr(res),
+                                            res.data_ptr() + off, _hip.stream_ptr()), "pu_noisy_channels")
+    h = res.cpu().numpy()
+    return h[:n].astype(bool), int(h[off:off + 4].view(np.int32)[0])
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+@pytest.mark.parametrize("n", [2, 3, 7, 8, 64, 255, 1000, 1024, 4095, 4096])
+def test_noisy_channels_device_matches_host(gpu, dt, n):
+    """pu_noisy_channels (get_noisier_channels' medfilt + ref_mad + comparison on the
+    device) equals the numpy / scipy decision bit for bit: noisy spectra with spikes, a
+    constant spectrum (MAD 0), quantised values (ties in the sorts and windows), both
+    parities of n - 1 (the two medians' middle-pair means)."""
+    rng = np.random.default_rng(n)
+    cases = [rng.normal(100, 1, n), np.full(n, 3.5), np.round(rng.normal(10, 2, n)) / 4,
+             rng.normal(0, 1e-3, n) + 1e6]
+    spike = rng.normal(50, 0.5, n)
+    spike[rng.choice(n, max(1, n // 20), replace=False)] += 40
+    cases.append(spike)
+    for c in cases:
+        spec = c.astype(dt)
+        mask, flag = _noisy_device(spec)
+        assert flag == 0
+        np.testing.assert_array_equal(mask, _noisy_host(spec))
+
+
+@pytest.mark.parametrize("bad", [np.nan, np.inf, -np.inf])
+def test_noisy_channels_nonfinite_flag(gpu, bad):
+    """A NaN / inf channel mean sets the flag (mask left alone); get_noisier_channels then
+    decides on the host, as the reference does."""
+    spec = np.random.default_rng(1).normal(100, 1, 512)
+    spec[17] = bad
+    mask, flag = _noisy_device(spec)
+    assert flag == 1
+    assert (mask == (7 != 0)).all()  # untouched (the fill byte)
+    x = np.random.default_rng(2).normal(0, 1, (64, 4096)).astype(np.float32)
+    x[5, 100] = bad
+    np.testing.assert_array_equal(C.get_noisier_channels(x), _noisy_host(x.mean(1)))
+
+
+def test_noisy_channels_wide_band_host_path(gpu):
+    """More channels than one workgroup decides (4097): the host path, same mask."""
+    x = np.random.default_rng(3).normal(0, 1, (4097, 256)).astype(np.float32)
+    x[100] += 5
+    np.testing.assert_array_equal(C.get_noisier_channels(x), _noisy_host(x.mean(1)))
