@@ -256,7 +256,7 @@ def _noisy_device(spec):
 
 
 @pytest.mark.parametrize("dt", [np.float32, np.float64])
-@pytest.mark.parametrize("n", [2, 3, 7, 8, 64, 255, 1000, 1024, 4095, 4096])
+@pytest.mark.parametrize("n", [2, 3, 7, 8, 64, 255, 1000, 1024, 1025, 1026, 4095, 4096])
 def test_noisy_channels_device_matches_host(gpu, dt, n):
     """pu_noisy_channels (get_noisier_channels' medfilt + ref_mad + comparison on the
     device) equals the numpy / scipy decision bit for bit: noisy spectra with spikes, a
