@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-OUT=gpurun_out/r03z
+OUT=${OUT:-gpurun_out/r03z}
 mkdir -p $OUT
 timeout -k 10 400 python -u -m pytest tests/test_gpu_clean.py tests/test_gpu_files.py -v -m gpu -x --timeout 200 --timeout-method thread -p no:cacheprovider > $OUT/gpu_tests_clean.log 2>&1 || exit $?
 timeout -k 10 300 python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-c3-strong > $OUT/bench.json 2> $OUT/bench.err || exit $?

@@ -294,3 +294,24 @@ def test_noisy_channels_wide_band_host_path(gpu):
     x = np.random.default_rng(3).normal(0, 1, (4097, 256)).astype(np.float32)
     x[100] += 5
     np.testing.assert_array_equal(C.get_noisier_channels(x), _noisy_host(x.mean(1)))
+
+
+@pytest.mark.parametrize("n", [1, 15, 16, 100, 8192, 65536, 65537, 200003])
+@pytest.mark.parametrize("padded", [False, True])
+def test_u8_row_sums_integer_path(gpu, n, padded):
+    """8-bit Σx (mean, modes 0/3) and Σx² (mode 4) by exact integer sums
+    (rowsum_u8_int_kernel: 16-byte aligned rows) equal numpy's float64 results bit for
+    bit; unaligned rows take the pairwise kernel, same bits."""
+    import torch
+    from pulsarutils import _hip
+    from pulsarutils.stats import _chunk_row_sums
+    rng = np.random.default_rng(n)
+    x = rng.integers(0, 256, (37, n), dtype=np.uint8)
+    x[3] = 255
+    ld = (n + 15) // 16 * 16 + 16 if padded else n
+    buf = torch.zeros((37, ld), dtype=torch.uint8, device="cuda")
+    buf[:, :n] = torch.from_numpy(x).cuda()
+    xd = buf[:, :n]
+    np.testing.assert_array_equal(C.channel_means_device(xd).cpu().numpy(), x.mean(1))
+    np.testing.assert_array_equal(_chunk_row_sums(xd, 3).cpu().numpy(), x.astype(float).sum(1))
+    np.testing.assert_array_equal(_chunk_row_sums(xd, 4).cpu().numpy(), (x.astype(float) ** 2).sum(1))
