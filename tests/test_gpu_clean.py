@@ -298,10 +298,9 @@ def test_noisy_channels_wide_band_host_path(gpu):
 
 @pytest.mark.parametrize("n", [1, 15, 16, 100, 8192, 65536, 65537, 200003])
 @pytest.mark.parametrize("padded", [False, True])
-def test_u8_row_sums_integer_path(gpu, n, padded):
-    """8-bit Σx (mean, modes 0/3) and Σx² (mode 4) by exact integer sums
-    (rowsum_u8_int_kernel: 16-byte aligned rows) equal numpy's float64 results bit for
-    bit; unaligned rows take the pairwise kernel, same bits."""
+def test_u8_row_sums_exact(gpu, n, padded):
+    """8-bit Σx (mean, modes 0/3) and Σx² (mode 4) equal numpy's float64 results bit for
+    bit, for contiguous and padded (ld > n) rows, full 8192-blocks and tails."""
     import torch
     from pulsarutils import _hip
     from pulsarutils.stats import _chunk_row_sums
