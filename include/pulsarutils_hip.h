@@ -72,12 +72,25 @@ int pu_plan_create(pu_plan **plan, int dtype, int acc, int64_t nchan, int64_t ns
                    const int64_t *shifts, int64_t ndm);
 /* Same, choosing the float32-accumulation strategy: ``group`` = channels summed into
  * one exact partial-sum row per distinct relative-shift vector:
- * 0 = default (PU_GROUP env, else the cheaper of 8 and 4 by the planner's cost model,
- * falling back to smaller groups / channel mode when the trial grid does not suit
- * them), 1 = channel mode, 2/4/8.  Float64
- * accumulation always runs channel mode (the reference's channel order). */
+ * 0 = default (the cheapest of the wide / tall shapes with G = 4 and 8 by the planner's
+ * cost model, falling back to smaller groups / channel mode when the trial grid does not
+ * suit them), 1 = channel mode, 2/4/8.  Float64 accumulation always runs channel mode
+ * (the reference's channel order).  = pu_plan_create_ex with opts {group, -1, 0, -1, -1}. */
 int pu_plan_create_grouped(pu_plan **plan, int dtype, int acc, int64_t nchan, int64_t nsamples,
                            const int64_t *shifts, int64_t ndm, int group);
+
+/* Explicit planner options (the production library reads no environment: every
+ * strategy choice is an argument here or a default).  -1 / 0 = automatic. */
+typedef struct pu_plan_opts {
+    int32_t group;          /* 0 auto, 1 channel mode, 2 / 4 / 8 */
+    int32_t shape;          /* subband workgroup shape: -1 auto, 0 wide, 1 pair, 2 tall */
+    int32_t lds_budget_kb;  /* 0: default (160 KiB subband, 64 KiB channel mode) */
+    int32_t u8_dma;         /* -1 auto (8-bit rows by LDS-DMA when n % 4 == 0), 0 global-memory build */
+    int32_t dt_major;       /* -1 auto item order, 0 time-tile major, 1 DM-tile major */
+    int32_t reserved[3];    /* zero */
+} pu_plan_opts;
+int pu_plan_create_ex(pu_plan **plan, int dtype, int acc, int64_t nchan, int64_t nsamples,
+                      const int64_t *shifts, int64_t ndm, const pu_plan_opts *opts);
 void pu_plan_destroy(pu_plan *plan);
 
 /* Device scratch bytes pu_plan_search needs (per-tile partial statistics). */

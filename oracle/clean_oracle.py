@@ -18,8 +18,10 @@ MAD_C = norm.ppf(3 / 4.)
 
 
 def mad(a, c=MAD_C):
-    """statsmodels 0.12.2 ``robust.scale.mad`` for 1-D input: median(|a - median(a)| / c)."""
-    a = np.asarray(a)
+    """statsmodels 0.12.2 ``robust.scale.mad`` for 1-D input: median(|a - median(a)| / c),
+    computed in float64 (``array_like(a, "a", ndim=None)``: default dtype np.double,
+    robust/scale.py:49)."""
+    a = np.asarray(a, dtype=np.double)
     center = np.apply_over_axes(np.median, a, 0) if a.size else 0.0
     return np.median(np.abs(a - center) / c, axis=0)
 

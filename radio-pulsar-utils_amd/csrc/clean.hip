@@ -885,9 +885,10 @@ __global__ void __launch_bounds__(256) median_final_kernel(MedState *st, const u
 // float64: numpy's mean dtype).  The host path it replaces did medfilt + ref_mad in numpy
 // after a read-back of spec; every step here keeps numpy's dtypes (NEP 50) and order:
 //   smooth = medfilt(spec, 7)           rank 3 of the zero-padded 7-window (T, exact)
-//   d = diff(spec)                      T
-//   m = median(d)                       T: the middle element, or (a + b) / 2 in T
-//   e = |d - m| / c                     |.| in T, then / c (numpy float64 scalar) in float64
+//   d = diff(spec)                      T, then float64: statsmodels 0.12.2's mad starts with
+//                                       array_like(a, dtype=np.double) (robust/scale.py:49)
+//   m = median(d)                       float64: the middle element, or (a + b) / 2
+//   e = |d - m| / c                     float64
 //   rm = median(e) / sqrt(2)            float64
 //   mask = spec > smooth + 5 rm         float64
 // A non-finite spec (NaN / inf: medfilt's and median's handling of them is left to
@@ -928,9 +929,7 @@ noisy_channels_kernel(const T *__restrict__ spec, int n, double c, uint8_t *__re
                       int32_t *__restrict__ flag)
 {
     __shared__ T sp[kNoisyMax];
-    __shared__ double buf[kNoisyMax];  // the sorted differences (T), then the sorted e (float64)
-    T *dv = reinterpret_cast<T *>(buf);
-    double *ev = buf;
+    __shared__ double ev[kNoisyMax];  // the sorted differences, then the sorted e (float64)
     const int tid = threadIdx.x;
     int nonfinite = 0;
     for (int i = tid; i < n; i += 1024) {
@@ -944,13 +943,14 @@ noisy_channels_kernel(const T *__restrict__ spec, int n, double c, uint8_t *__re
     }
     int m = 1;
     while (m < n - 1) m <<= 1;
-    for (int i = tid; i < m; i += 1024) dv[i] = i < n - 1 ? T(sp[i + 1] - sp[i]) : T(INFINITY);
+    // the differences in T (np.diff of the T spectrum), then exactly widened to float64
+    for (int i = tid; i < m; i += 1024) ev[i] = i < n - 1 ? (double)T(sp[i + 1] - sp[i]) : INFINITY;
     __syncthreads();
-    bitonic_sort_lds(dv, m);
-    const T med = median_sorted(dv, n - 1);
-    __syncthreads();  // every thread has read the median before buf is overwritten
+    bitonic_sort_lds(ev, m);
+    const double med = median_sorted(ev, n - 1);
+    __syncthreads();  // every thread has read the median before ev is overwritten
     for (int i = tid; i < m; i += 1024)
-        ev[i] = i < n - 1 ? (double)T(fabs(T(sp[i + 1] - sp[i]) - med)) / c : INFINITY;
+        ev[i] = i < n - 1 ? fabs((double)T(sp[i + 1] - sp[i]) - med) / c : INFINITY;
     __syncthreads();
     bitonic_sort_lds(ev, m);
     const double rm = median_sorted(ev, n - 1) / 1.4142135623730951;  // np.sqrt(2)
@@ -1000,7 +1000,7 @@ int row_sums_t(const void *x, int64_t nrows, int64_t n, int64_t ld, const void *
                           (MODE != 2 || reinterpret_cast<uintptr_t>(scale) % 16 == 0);
         // MODE 2: R rows per workgroup share the scale pairs (PU_CLEAN_SCALE_ROWS: 4, 8, 16)
         int rsel = kScaleRows;
-        if (const char *e = getenv("PU_CLEAN_SCALE_ROWS")) rsel = atoi(e);
+        rsel = pu::knob("PU_CLEAN_SCALE_ROWS", rsel);
         auto go = [&](auto rc_) {
             constexpr int R = MODE == 2 ? decltype(rc_)::value : 1;
             const int64_t ngroups = (nrows + R - 1) / R;
@@ -1067,10 +1067,7 @@ int pick_vec(const void *p, int64_t ld, int vmax)
 // PU_CLEAN_VMAX overrides both (1, 2 or 4).
 int vec_max(size_t elem, int dflt)
 {
-    const int env = [] {
-        const char *e = getenv("PU_CLEAN_VMAX");
-        return e ? atoi(e) : 0;
-    }();
+    const int env = pu::knob("PU_CLEAN_VMAX", 0);
     const int v = env > 0 ? env : dflt;
     const int w = v >= 4 ? 4 : v >= 2 ? 2 : 1;
     return elem >= 8 && w > 2 ? 2 : w;
@@ -1096,10 +1093,7 @@ int col_means_t(const void *x, int64_t nrows, int64_t n, int64_t ld, const uint8
 {
     if constexpr (sizeof(Tin) == 1) {
         // 8-bit input: exact integer sums by row segments (PU_COLSEG=0: the sequential kernel)
-        static const bool seg = [] {
-            const char *e = getenv("PU_COLSEG");
-            return !e || atoi(e) != 0;
-        }();
+        static const bool seg = pu::knob("PU_COLSEG", 1) != 0;
         const int nseg = (int)((nrows + kColSegRows - 1) / kColSegRows);
         if (seg && nseg <= kColSegMax && n % 8 == 0 && ld % 8 == 0 && reinterpret_cast<uintptr_t>(x) % 8 == 0) {
             hipLaunchKernelGGL(colsum_u8_seg_kernel, dim3(blocks_for(n / 8, 256), nseg), dim3(256), 0, s,
@@ -1113,7 +1107,7 @@ int col_means_t(const void *x, int64_t nrows, int64_t n, int64_t ld, const uint8
     const int v = pick_vec<Tin>(x, ld, vec_max(sizeof(Tin), 4));
     // bytes of rows in flight per lane and register buffer (PU_CLEAN_BATCH: 128, 256 or 512)
     int bb = 256;  // C4 sweep (profiles/r02_clean/): f32 V=4 190 us vs 212 us at 128 B
-    if (const char *e = getenv("PU_CLEAN_BATCH")) bb = atoi(e);
+    bb = pu::knob("PU_CLEAN_BATCH", bb);
     return column_launches<Tin>(v, n, [&](auto vc, int64_t col0, int64_t ncols) {
         constexpr int V = decltype(vc)::value;
         if (bb >= 512)
@@ -1132,10 +1126,7 @@ int col_means_t(const void *x, int64_t nrows, int64_t n, int64_t ld, const uint8
 // 542 -> 481 us), off for float input (606 vs 623 us); PU_CLEAN_NT=0/1 overrides.
 bool nt_stores(size_t elem)
 {
-    const int env = [] {
-        const char *e = getenv("PU_CLEAN_NT");
-        return e ? atoi(e) : -1;
-    }();
+    const int env = pu::knob("PU_CLEAN_NT", -1);
     return env >= 0 ? env != 0 : elem == 1;
 }
 
@@ -1158,7 +1149,7 @@ int renorm_apply_t(const void *x, int64_t nchan, int64_t n, int64_t ld, const do
         const bool nt = nt_stores(sizeof(Tin));
         // bytes of rows in flight per lane and register buffer (PU_APPLY_BATCH)
         int bb = kBatchBytes;
-        if (const char *e = getenv("PU_APPLY_BATCH")) bb = atoi(e);
+        bb = pu::knob("PU_APPLY_BATCH", bb);
         auto pick = [&](auto ntc, auto zc) {
             constexpr bool NT = decltype(ntc)::value, Z = decltype(zc)::value;
             if (bb >= 512) go(apply_kernel<Tin, V, NT, Z, 512>);
@@ -1222,10 +1213,7 @@ int pu_gaussian_filter1d(const double *x, int64_t n, const double *w, int64_t r,
 {
     PU_REQUIRE(x && w && out && n > 0 && r >= 0, "pu_gaussian_filter1d: bad arguments");
     if (r <= kGaussMaxR) {
-        static const bool single = [] {
-            const char *e = getenv("PU_GAUSS_SINGLE");  // the one-output form, for A/B
-            return e && atoi(e) != 0;
-        }();
+        static const bool single = pu::knob("PU_GAUSS_SINGLE", 0) != 0;  // the one-output form, for A/B
         if (single) {
             const size_t lds = (size_t)(r + 1 + 256 + 2 * r) * sizeof(double);
             hipLaunchKernelGGL(gauss_lds_kernel, dim3(blocks_for(n, 256)), dim3(256), lds, pu::as_stream(stream), x,
@@ -1319,7 +1307,7 @@ int pu_median(const double *x, int64_t n, double *out, void *ws, size_t ws_bytes
     // a few elements per thread: fewer workgroups to flush LDS bins to the global histogram
     // (PU_MEDIAN_GRID: most workgroups per pass, tuning)
     int64_t gmax = 256;
-    if (const char *e = getenv("PU_MEDIAN_GRID")) gmax = std::max(1, atoi(e));
+    gmax = std::max(1, pu::knob("PU_MEDIAN_GRID", (int)gmax));
     const unsigned grid = std::min<int64_t>(gmax, std::max<int64_t>(1, (n + 1023) / 1024));
     for (int p = 0; p < kMedPasses; ++p)
         hipLaunchKernelGGL(median_hist_kernel, dim3(grid), dim3(256), 0, s, x, n, st, hist, p);

@@ -35,6 +35,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <type_traits>
 #include <vector>
 
@@ -1483,7 +1484,20 @@ struct SubHost {
 
 }  // namespace
 
+// Per-plan lock: a plan holds mutable per-call state (timing events and the launch
+// counter, the pinned certification copy and the last call's certification outcome),
+// and cached plans are shared across threads (ctypes releases the GIL).  Every entry
+// point that launches or reads that state holds it for the whole call.  Copying a plan
+// (reset_tables) keeps the destination's mutex.
+struct PlanLock {
+    std::mutex m;
+    PlanLock() = default;
+    PlanLock(const PlanLock &) {}
+    PlanLock &operator=(const PlanLock &) { return *this; }
+};
+
 struct pu_plan {
+    mutable PlanLock lock;
     SubHost host;
     int dtype = 0, acc = 0, variant = 0;
     int64_t nchan = 0, n = 0, ndm = 0;
@@ -1501,6 +1515,7 @@ struct pu_plan {
     int64_t exec_adds = 0, lds_traffic = 0;  // per launch (measurement: bench.py roofline)
     int64_t nstages = 0;
     int dt_major = 0;  // subband item order (SubArgs::dt_major)
+    int opt_u8_dma = -1, opt_dt_major = -1;  // pu_plan_opts (planner inputs)
     i32x4 *d_tiles = nullptr, *d_stages = nullptr;
     i32x2 *d_tile_stages = nullptr;
     int32_t *d_slots = nullptr;
@@ -1515,8 +1530,6 @@ struct pu_plan {
     std::vector<int64_t> shifts;
     CertState *h_cert = nullptr;
     int64_t cert_rechecked = 0, cert_nan = 0, cert_why[3] = {0, 0, 0}, cert_us = 0;
-    void *rc_buf = nullptr;  // recheck scratch (series, pu_series_stats workspace, shifts, indices)
-    size_t rc_bytes = 0;
 };
 
 namespace {
@@ -1668,7 +1681,6 @@ void free_plan(pu_plan *p)
     (void)hipFree(p->d_recs);
     (void)hipFree(p->d_stamps);
     if (p->h_cert) (void)hipHostFree(p->h_cert);
-    (void)hipFree(p->rc_buf);
     delete p;
 }
 
@@ -1814,7 +1826,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     // 8-bit rows are staged as bytes by LDS-DMA when every row window starts on a dword
     // (n % 4 == 0; the row's misalignment base % 4 is folded into the slot sources)
     bool dma8 = p->dtype == PU_U8 && n % 4 == 0;
-    if (const char *env = getenv("PU_U8_DMA")) dma8 = dma8 && atoi(env) != 0;
+    dma8 = dma8 && pu::knob("PU_U8_DMA", p->opt_u8_dma) != 0;
     const bool dma = p->dtype == PU_F32 || dma8;
     const int64_t eb = dma8 ? 1 : 4;  // bytes per staged raw element
     const bool pack_cover = n < (int64_t(1) << 24);  // row bases fit 24 bits: covers above them
@@ -2086,7 +2098,8 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     // for the time-tile-major order too cost C3 1.1 % - 1109 vs 1122 ms.)
     const int64_t ntt_plan = (n + TT - 1) / TT;
     bool dt_major = (int64_t)ndt * ntt_plan < kDtMajorItems;
-    if (const char *env = getenv("PU_DT_MAJOR")) dt_major = atoi(env) != 0;
+    if (p->opt_dt_major >= 0) dt_major = p->opt_dt_major != 0;
+    dt_major = pu::knob("PU_DT_MAJOR", dt_major ? 1 : 0) != 0;
     if (dt_major) {
         std::vector<int> perm((size_t)ndt);
         for (int t = 0; t < ndt; ++t) perm[t] = t;
@@ -2179,6 +2192,8 @@ void reset_tables(pu_plan *p)
     keep.K = p->K;
     keep.TT = p->TT;
     keep.ntt = p->ntt;
+    keep.opt_u8_dma = p->opt_u8_dma;
+    keep.opt_dt_major = p->opt_dt_major;
     (void)hipFree(p->d_first);
     (void)hipFree(p->d_count);
     (void)hipFree(p->d_rowlen);
@@ -2255,8 +2270,8 @@ int launch_finalize(pu_plan *p, const void *part, double *mx, double *sd, double
 // gives every trial the reference's NaN result; other flagged trials are recomputed
 // exactly - their float64 channel-order series (the reference's bit for bit, by a direct
 // gather: ~1 ms per trial at C3, far below a channel-mode sub-plan's cost for the
-// few trials a search flags) + pu_series_stats - in batches that fit ~1 GiB of scratch
-// kept with the plan.
+// few trials a search flags) + pu_series_stats - in batches that fit ~1 GiB of
+// stream-ordered scratch allocated for the call.
 int resolve_flagged(pu_plan *p, const void *data, int64_t ld, double *mx, double *sd, double *snr, int32_t *win,
                     char *ws, hipStream_t s)
 {
@@ -2307,14 +2322,20 @@ int resolve_flagged(pu_plan *p, const void *data, int64_t ld, double *mx, double
     const size_t sws_b = (pu_series_stats_workspace_bytes(B, n) + 255) & ~size_t(255);
     const size_t sh_b = ((size_t)B * nchan * sizeof(int64_t) + 255) & ~size_t(255);
     const size_t need = plane_b + sws_b + sh_b + (size_t)B * sizeof(int32_t);
-    if (p->rc_bytes < need) {  // scratch kept with the plan, grown on demand
-        (void)hipFree(p->rc_buf);
-        p->rc_buf = nullptr;
-        p->rc_bytes = 0;
-        PU_TRY_HIP(hipMalloc(&p->rc_buf, need));
-        p->rc_bytes = need;
-    }
-    char *sc = reinterpret_cast<char *>(p->rc_buf);
+    // per-call scratch, stream-ordered (no device-wide synchronisation, nothing held
+    // with the plan between calls); freed on every return path
+    void *rc_buf = nullptr;
+    PU_TRY_HIP(hipMallocAsync(&rc_buf, need, s));
+    struct Scratch {
+        void *b;
+        hipStream_t s;
+        ~Scratch()
+        {
+            (void)hipFreeAsync(b, s);
+            (void)hipStreamSynchronize(s);
+        }
+    } scratch{rc_buf, s};
+    char *sc = reinterpret_cast<char *>(rc_buf);
     double *plane = reinterpret_cast<double *>(sc);
     void *sws = sc + plane_b;
     int64_t *d_sh = reinterpret_cast<int64_t *>(sc + plane_b + sws_b);
@@ -2345,10 +2366,17 @@ int resolve_flagged(pu_plan *p, const void *data, int64_t ld, double *mx, double
 
 extern "C" {
 
-int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t n, const int64_t *shifts,
-                           int64_t ndm, int group)
+int pu_plan_create_ex(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t n, const int64_t *shifts,
+                      int64_t ndm, const pu_plan_opts *opts)
 {
     PU_REQUIRE(out != nullptr, "pu_plan_create: out is NULL");
+    PU_REQUIRE(opts != nullptr, "pu_plan_create_ex: opts is NULL");
+    const int group = opts->group;
+    PU_REQUIRE(opts->shape >= -1 && opts->shape <= 2, "pu_plan_create_ex: shape %d not in {-1, 0, 1, 2}", opts->shape);
+    PU_REQUIRE(opts->lds_budget_kb == 0 || (opts->lds_budget_kb >= 8 && opts->lds_budget_kb <= 160),
+               "pu_plan_create_ex: lds_budget_kb %d not 0 or in [8, 160]", opts->lds_budget_kb);
+    PU_REQUIRE(opts->u8_dma >= -1 && opts->u8_dma <= 1 && opts->dt_major >= -1 && opts->dt_major <= 1,
+               "pu_plan_create_ex: u8_dma / dt_major must be -1, 0 or 1");
     *out = nullptr;
     const int v = pick_variant(dtype, acc);
     PU_REQUIRE(v >= 0, "pu_plan_create: unsupported dtype %d", dtype);
@@ -2374,22 +2402,26 @@ int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int
     p->K = E * 4;
     p->TT = 64 * p->K;
     p->ntt = (int)((n + p->TT - 1) / p->TT);
+    p->opt_u8_dma = opts->u8_dma < 0 ? 1 : opts->u8_dma;
+    p->opt_dt_major = opts->dt_major;
 
-    // LDS budget per workgroup (channel / subband mode); PU_LDS_BUDGET_KB overrides (tuning)
-    // subband workgroup shape: PU_SUB_SHAPE 0 = wide (1 WG/CU), 1 = pair (2 WGs/CU),
-    // 2 = tall (256 trials x 256 samples, 1 WG/CU)
-    int shape = SUB_WIDE;
-    if (const char *env = getenv("PU_SUB_SHAPE")) shape = std::clamp(atoi(env), 0, 2);
+    // subband workgroup shape: 0 = wide (1 WG/CU), 1 = pair (2 WGs/CU), 2 = tall (256
+    // trials x 256 samples, 1 WG/CU); -1 = the cost model's choice among wide and tall.
+    // LDS budget per workgroup (channel / subband mode).  (Diagnostic build: PU_SUB_SHAPE,
+    // PU_LDS_BUDGET_KB and PU_GROUP override the options, for A/B sweeps.)
+    const int shape_opt = pu::knob("PU_SUB_SHAPE", opts->shape);
+    const int budget_kb = pu::knob("PU_LDS_BUDGET_KB", opts->lds_budget_kb);
+    int shape = shape_opt < 0 ? SUB_WIDE : std::clamp(shape_opt, 0, 2);
     size_t budget = kLdsBudget, sub_budget = shape == SUB_PAIR ? 80 * 1024 : 160 * 1024;
-    if (const char *env = getenv("PU_LDS_BUDGET_KB")) budget = sub_budget = (size_t)std::max(8, atoi(env)) * 1024;
-    // group size: explicit, else PU_GROUP, else 4; float32 accumulation only (the
-    // float64 modes keep the reference's sequential channel order)
-    int G = group;
+    if (budget_kb > 0) budget = sub_budget = (size_t)std::max(8, budget_kb) * 1024;
+    // group size: explicit, else the automatic choice (G = 4 where it is not calibrated);
+    // float32 accumulation only (the float64 modes keep the reference's sequential
+    // channel order)
+    int G = pu::knob("PU_GROUP", group);
     bool auto_g = false;
     if (G == 0) {
         G = 4;
-        if (const char *env = getenv("PU_GROUP")) G = atoi(env);
-        else auto_g = !kVariants[v].acc_f64 && nchan > 8;
+        auto_g = !kVariants[v].acc_f64 && nchan > 8;
     }
     G = std::min(G, 8);
     if (kVariants[v].acc_f64) G = 1;
@@ -2397,7 +2429,7 @@ int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int
     // The automatic choice is calibrated on the wide shape with DMA-staged rows (f32, or
     // u8 with n % 4 == 0); elsewhere the default stays G = 4.
     const bool dma_rows = dtype == PU_F32 || (dtype == PU_U8 && n % 4 == 0);
-    if (auto_g && (shape != SUB_WIDE || !dma_rows || getenv("PU_LDS_BUDGET_KB"))) auto_g = false;
+    if (auto_g && (shape != SUB_WIDE || !dma_rows || budget_kb > 0)) auto_g = false;
     int rc = PU_EUNSUPPORTED;
     if (auto_g) {
         // Default group size: plan G = 8 and G = 4 on the host and keep the cheaper by the
@@ -2418,6 +2450,8 @@ int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int
             q->K = p->K;
             q->TT = p->TT;
             q->ntt = p->ntt;
+            q->opt_u8_dma = p->opt_u8_dma;
+            q->opt_dt_major = p->opt_dt_major;
             return q;
         };
         // Round 3: the tall shape (256 trials x 256 samples) competes too, with G = 4 and 8.
@@ -2425,7 +2459,7 @@ int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int
         // C2 tall G4 14.92 ms (wide G4 15.23, tall G8 20.19), C3 tall G8 1042 ms (wide G8
         // 1114; 625 trials 125.6 vs 132.4, tall G4 135.8), C5 tall G4 0.365 (wide 0.374),
         // C4 wide G4 0.581 (100 trials: tall 0.662).  PU_SUB_SHAPE pins the shape.
-        const bool try_tall = !getenv("PU_SUB_SHAPE");
+        const bool try_tall = shape_opt < 0;
         pu_plan *q = fresh(), *t4 = try_tall ? fresh() : nullptr, *t8 = try_tall ? fresh() : nullptr;
         const int rc8 = plan_sub(q, shifts, 8, shape, sub_budget);
         const int rc4 = plan_sub(p, shifts, 4, shape, sub_budget);
@@ -2471,6 +2505,17 @@ int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int
     return PU_OK;
 }
 
+int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t n, const int64_t *shifts,
+                           int64_t ndm, int group)
+{
+    pu_plan_opts o{};
+    o.group = group;
+    o.shape = -1;
+    o.u8_dma = -1;
+    o.dt_major = -1;
+    return pu_plan_create_ex(out, dtype, acc, nchan, n, shifts, ndm, &o);
+}
+
 int pu_plan_create(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t n, const int64_t *shifts, int64_t ndm)
 {
     return pu_plan_create_grouped(out, dtype, acc, nchan, n, shifts, ndm, 0);
@@ -2481,6 +2526,7 @@ void pu_plan_destroy(pu_plan *p) { free_plan(p); }
 int pu_plan_enable_timing(pu_plan *p, int nslots)
 {
     PU_REQUIRE(p != nullptr && nslots >= 0 && nslots <= 65536, "pu_plan_enable_timing: bad arguments");
+    std::lock_guard<std::mutex> guard(p->lock.m);
     destroy_events(p);
     for (auto *v : {&p->ev_start, &p->ev_stop}) {
         v->assign((size_t)nslots, nullptr);
@@ -2493,6 +2539,7 @@ int pu_plan_enable_timing(pu_plan *p, int nslots)
 int pu_plan_stamps(pu_plan *p, int64_t *out, int n)
 {
     PU_REQUIRE(p != nullptr && out != nullptr, "pu_plan_stamps: bad arguments");
+    std::lock_guard<std::mutex> guard(p->lock.m);
 #ifdef PU_STAMPS
     if (!p->d_stamps) {
         PU_TRY_HIP(hipMalloc((void **)&p->d_stamps, 8 * sizeof(uint64_t)));
@@ -2515,6 +2562,7 @@ int pu_plan_stamps(pu_plan *p, int64_t *out, int n)
 int pu_plan_kernel_times(pu_plan *p, float *ms, int n)
 {
     PU_REQUIRE(p != nullptr && ms != nullptr, "pu_plan_kernel_times: bad arguments");
+    std::lock_guard<std::mutex> guard(p->lock.m);
     const int64_t have = std::min<int64_t>(p->launches, (int64_t)p->ev_start.size());
     const int m = (int)std::min<int64_t>(n, have);
     for (int i = 0; i < m; ++i) {
@@ -2534,6 +2582,7 @@ size_t pu_plan_workspace_bytes(const pu_plan *p)
 int pu_plan_info(const pu_plan *p, int64_t *info, int n)
 {
     if (!p || !info) return 0;
+    std::lock_guard<std::mutex> guard(p->lock.m);
     const int64_t v[] = {p->ndm, p->ndt, p->ntt, p->group > 1 ? with_shape(p->shape, [](auto c) { return decltype(c)::T; }) : kTPT, p->TT, p->ncc,
                          p->row_stride, (int64_t)p->lds_bytes, kVariants[p->variant].acc_f64, p->max_spread,
                          p->group, p->nslots_total, p->nstages, (int64_t)p->slot_bytes, p->raw_stride,
@@ -2576,6 +2625,7 @@ int pu_plan_search_tiles(pu_plan *p, const void *data, int64_t ld, int64_t tt_be
 {
     int rc = check_data(p, data, ld);
     if (rc) return rc;
+    std::lock_guard<std::mutex> guard(p->lock.m);
     PU_REQUIRE(0 <= tt_begin && tt_begin <= tt_end && tt_end <= p->ntt,
                "pu_plan_search_tiles: tile range [%lld, %lld) outside [0, %d)", (long long)tt_begin,
                (long long)tt_end, p->ntt);
@@ -2593,6 +2643,7 @@ int pu_plan_finalize(pu_plan *p, const void *data, int64_t ld, double *max_out, 
 {
     int rc = check_data(p, data, ld);
     if (rc) return rc;
+    std::lock_guard<std::mutex> guard(p->lock.m);
     PU_REQUIRE(max_out && std_out && snr_out && rebin_out, "pu_plan_finalize: NULL output");
     PU_REQUIRE(workspace && ws_bytes >= pu_plan_workspace_bytes(p) && reinterpret_cast<uintptr_t>(workspace) % 8 == 0,
                "pu_plan_finalize: workspace too small or not 8-byte aligned");
@@ -2608,6 +2659,7 @@ int pu_plan_search(pu_plan *p, const void *data, int64_t ld, double *max_out, do
 {
     int rc = check_data(p, data, ld);
     if (rc) return rc;
+    std::lock_guard<std::mutex> guard(p->lock.m);
     PU_REQUIRE(max_out && std_out && snr_out && rebin_out, "pu_plan_search: NULL output");
     PU_REQUIRE(workspace && ws_bytes >= pu_plan_workspace_bytes(p) && reinterpret_cast<uintptr_t>(workspace) % 8 == 0,
                "pu_plan_search: workspace too small or not 8-byte aligned");
@@ -2626,6 +2678,7 @@ int pu_plan_dedisperse(pu_plan *p, const void *data, int64_t ld, void *plane, in
 {
     int rc = check_data(p, data, ld);
     if (rc) return rc;
+    std::lock_guard<std::mutex> guard(p->lock.m);
     PU_REQUIRE(plane != nullptr, "pu_plan_dedisperse: plane is NULL");
     PU_REQUIRE(ld_plane >= p->n, "pu_plan_dedisperse: ld_plane < nsamples");
     DedispArgs a = make_args(p, data, ld);

@@ -4,6 +4,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 
 #include "pulsarutils_hip.h"
@@ -52,6 +53,30 @@ inline size_t elem_size(int dtype)
     case PU_I64: return 8;
     default: return 0;
     }
+}
+
+// Tuning knobs for A/B experiments (group size, workgroup shape, batch sizes ...): read
+// from the environment ONLY in the diagnostic build (make stamps: -DPU_STAMPS,
+// libpulsarutils_hip_stamps.so).  The production library ignores the environment and
+// always runs its defaults or the explicit plan-create arguments, so a stray PU_* in a
+// user's environment cannot change a kernel (the reference is configured by kwargs only).
+inline bool knob_set(const char *name)
+{
+#ifdef PU_STAMPS
+    return getenv(name) != nullptr;
+#else
+    (void)name;
+    return false;
+#endif
+}
+
+inline int knob(const char *name, int dflt)
+{
+#ifdef PU_STAMPS
+    if (const char *e = getenv(name)) return atoi(e);
+#endif
+    (void)name;
+    return dflt;
 }
 
 inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }

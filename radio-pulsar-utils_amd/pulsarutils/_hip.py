@@ -29,6 +29,7 @@ SIGNATURES = {
     "pu_shift_table": (_i32, [_i64, _vp, _i64, _f64, _f64, _f64, _vp]),
     "pu_plan_create": (_i32, [ctypes.POINTER(_vp), _i32, _i32, _i64, _i64, _vp, _i64]),
     "pu_plan_create_grouped": (_i32, [ctypes.POINTER(_vp), _i32, _i32, _i64, _i64, _vp, _i64, _i32]),
+    "pu_plan_create_ex": (_i32, [ctypes.POINTER(_vp), _i32, _i32, _i64, _i64, _vp, _i64, _vp]),
     "pu_plan_destroy": (None, [_vp]),
     "pu_plan_workspace_bytes": (_sz, [_vp]),
     "pu_plan_search": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
@@ -72,6 +73,15 @@ INFO_FIELDS = ("ndm", "dm_tiles", "time_tiles", "trials_per_tile", "time_tile", 
 
 class HipBackendError(RuntimeError):
     pass
+
+
+class PlanOpts(ctypes.Structure):
+    """``pu_plan_opts`` (include/pulsarutils_hip.h): the planner's explicit options."""
+    _fields_ = [("group", ctypes.c_int32), ("shape", ctypes.c_int32), ("lds_budget_kb", ctypes.c_int32),
+                ("u8_dma", ctypes.c_int32), ("dt_major", ctypes.c_int32), ("reserved", ctypes.c_int32 * 3)]
+
+
+SHAPES = {"wide": 0, "pair": 1, "tall": 2}
 
 
 _SRC_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
@@ -196,17 +206,26 @@ def to_device(a, allowed=(PU_U8, PU_F32, PU_F64), device=None):
 class Plan:
     """Owning wrapper of a ``pu_plan`` (dedispersion tiling + device metadata)."""
 
-    def __init__(self, dtype_code_, acc, nchan, nsamples, shifts, group=0):
+    def __init__(self, dtype_code_, acc, nchan, nsamples, shifts, group=0, shape=None, lds_budget_kb=0,
+                 u8_dma=None, dt_major=None):
         """``group``: channels summed per group row (0 = library default, 1 = channel
-        mode, 2/4/8); float64 accumulation always uses channel mode."""
+        mode, 2/4/8); float64 accumulation always uses channel mode.  ``shape``: subband
+        workgroup shape ("wide", "pair", "tall" or 0/1/2; None = the cost model's choice);
+        ``lds_budget_kb``: LDS per workgroup (0 = default); ``u8_dma``: False builds 8-bit
+        slots from global memory instead of LDS-DMA'd rows; ``dt_major``: work-item order
+        (None = automatic).  These are the planner's only inputs (pu_plan_create_ex): the
+        library reads no environment."""
         require_gpu()
         sh = np.ascontiguousarray(shifts, dtype=np.int64)
         if sh.ndim != 2 or sh.shape[1] != int(nchan):
             raise ValueError(f"shift table must be (ndm, {nchan}) int64, got shape {sh.shape}")
         ndm = sh.shape[0]
+        opts = PlanOpts(group=int(group), shape=-1 if shape is None else int(SHAPES.get(shape, shape)),
+                        lds_budget_kb=int(lds_budget_kb), u8_dma=-1 if u8_dma is None else int(bool(u8_dma)),
+                        dt_major=-1 if dt_major is None else int(bool(dt_major)))
         h = ctypes.c_void_p()
-        check(lib().pu_plan_create_grouped(ctypes.byref(h), dtype_code_, acc, nchan, nsamples,
-                                           sh.ctypes.data_as(ctypes.c_void_p), ndm, int(group)),
+        check(lib().pu_plan_create_ex(ctypes.byref(h), dtype_code_, acc, nchan, nsamples,
+                                      sh.ctypes.data_as(ctypes.c_void_p), ndm, ctypes.byref(opts)),
               "pu_plan_create")
         self._h = h
         self.dtype_code = dtype_code_

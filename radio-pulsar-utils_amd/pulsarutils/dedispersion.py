@@ -11,10 +11,11 @@ Device-resident use (no PCIe copies): pass a CUDA ``torch.Tensor`` as ``data`` t
 Accumulation: ``acc='native'`` (default) sums uint8 exactly in
 float32, float32 in float32 (stated tolerance) and float64 in float64 (bit-exact);
 ``acc='f64'`` sums everything in float64 in channel order, bit-identical to the
-reference's dedispersed series.  The environment variable ``PULSARUTILS_ACC``
-changes the default.
+reference's dedispersed series.  Nothing here or in the library is configured by the
+environment (:func:`planner_options` scopes explicit planner options).
 """
 import collections
+import contextlib
 import hashlib
 import os
 import threading
@@ -30,7 +31,7 @@ _ACC = {"native": _hip.PU_ACC_NATIVE, "f32": _hip.PU_ACC_F32, "f64": _hip.PU_ACC
 
 
 def _acc_code(acc):
-    acc = acc or os.environ.get("PULSARUTILS_ACC", "native")
+    acc = acc or "native"
     try:
         return _ACC[acc]
     except KeyError:
@@ -121,13 +122,30 @@ def _prepare_data(data):
 
 
 # Plans (tiling + device metadata) of recent calls, so repeated numpy-API calls on the same
-# shape and trial grid skip the host planner (~35 ms at C2).  A plan is read-only during a
-# launch (workspace and outputs are per call), so sharing one is safe.  The key holds the
-# planner's tuning variables, which are read when a plan is built.
+# shape and trial grid skip the host planner (~35 ms at C2).  Sharing one across threads
+# is safe: workspace and outputs are per call, and the library holds a per-plan lock
+# across each launch + finalize + certification (pu_plan's mutable state: timing events,
+# the certification read-back).  The key holds the planner options in force
+# (:func:`planner_options`).
 _PLAN_CACHE = collections.OrderedDict()
 _PLAN_CACHE_SIZE = 4
 _PLAN_LOCK = threading.Lock()
-_PLAN_ENV = ("PU_SUB_SHAPE", "PU_LDS_BUDGET_KB", "PU_GROUP", "PU_U8_DMA")
+_PLAN_OPTS = threading.local()
+
+
+@contextlib.contextmanager
+def planner_options(**opts):
+    """Planner options for the plans the drop-in functions build in this thread (the
+    keyword arguments of :class:`pulsarutils._hip.Plan`: ``group``, ``shape``,
+    ``lds_budget_kb``, ``u8_dma``, ``dt_major``).  The reference has no such knob; the
+    defaults are the library's automatic choices.  Explicit and scoped: nothing is read
+    from the environment."""
+    old = getattr(_PLAN_OPTS, "opts", {})
+    _PLAN_OPTS.opts = {**old, **opts}
+    try:
+        yield
+    finally:
+        _PLAN_OPTS.opts = old
 
 
 def _plan_for(x, shifts, acc, ident=None):
@@ -137,15 +155,16 @@ def _plan_for(x, shifts, acc, ident=None):
     if ident is None:
         shifts = np.ascontiguousarray(shifts, dtype=np.int64)
         ident = (hashlib.sha1(shifts.tobytes()).hexdigest(), shifts.shape)
+    opts = dict(getattr(_PLAN_OPTS, "opts", {}))
     key = (_hip.dtype_code(x.dtype), acc, x.shape[0], x.shape[1], x.device.index, ident,
-           tuple(os.environ.get(k) for k in _PLAN_ENV))
+           tuple(sorted(opts.items())))
     with _PLAN_LOCK:
         plan = _PLAN_CACHE.get(key)
         if plan is not None:
             _PLAN_CACHE.move_to_end(key)
             return plan
     sh = shifts() if callable(shifts) else shifts
-    plan = _hip.Plan(key[0], acc, x.shape[0], x.shape[1], sh)
+    plan = _hip.Plan(key[0], acc, x.shape[0], x.shape[1], sh, **opts)
     with _PLAN_LOCK:
         _PLAN_CACHE[key] = plan
         while len(_PLAN_CACHE) > _PLAN_CACHE_SIZE:

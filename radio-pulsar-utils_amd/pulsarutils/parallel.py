@@ -83,6 +83,21 @@ class PlanSearcher:
             o.record_stream(stream)
 
 
+_MASKED = {}  # (device index, reserved CUs) -> MaskedStream, kept for the process
+
+
+def _masked_stream(reserve, dev):
+    """The CU-masked compute stream for ``reserve`` CUs on ``dev``, created once and kept
+    alive for the process: tensors record_stream'ed onto it (the searcher's workspace and
+    outputs) are freed later by the caching allocator, which then records an event on
+    this stream - so it must outlive them."""
+    from ._hip import MaskedStream
+    key = (dev.index, int(reserve))
+    if key not in _MASKED:
+        _MASKED[key] = MaskedStream(reserve, dev)
+    return _MASKED[key]
+
+
 def pipelined_broadcast_search(data, plan, out=None, workspace=None, src=0, chunks=8, group=None, searcher=None,
                                reserve_cus=0):
     """Broadcast ``data`` from ``src`` in time chunks while searching it with ``plan``.
@@ -132,8 +147,7 @@ def pipelined_broadcast_search(data, plan, out=None, workspace=None, src=0, chun
         comm.wait_stream(cur)
         comp.wait_stream(cur)
         if world > 1 and reserve_cus > 0 and searcher is not None and len(bounds) > 1:
-            from ._hip import MaskedStream
-            masked = MaskedStream(reserve_cus, dev)
+            masked = _masked_stream(reserve_cus, dev)
             masked.stream.wait_stream(cur)
     else:
         cur = comm = comp = None
@@ -183,8 +197,6 @@ def pipelined_broadcast_search(data, plan, out=None, workspace=None, src=0, chun
             if masked is not None:
                 searcher.streams_done(masked.stream)
         cur.wait_stream(comp)
-        if masked is not None:
-            masked.stream.synchronize()  # before the stream is destroyed with ``masked``
     return res
 
 

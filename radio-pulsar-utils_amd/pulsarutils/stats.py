@@ -23,8 +23,12 @@ MAD_C = norm.ppf(3 / 4.)
 
 
 def mad(a, c=MAD_C, axis=0, center=np.median):
-    """statsmodels 0.12.2 ``robust.mad``: ``median(|a - center(a)| / c)`` along ``axis``."""
-    a = np.asarray(a)
+    """statsmodels 0.12.2 ``robust.mad``: ``median(|a - center(a)| / c)`` along ``axis``.
+
+    The input is converted to float64 first, as statsmodels' ``array_like(a, "a",
+    ndim=None)`` does (its default ``dtype=np.double``, robust/scale.py:49), so a float32
+    input's median and deviations are float64."""
+    a = np.asarray(a, dtype=np.double)
     if callable(center) and a.size:
         center = np.apply_over_axes(center, a, axis)
     else:

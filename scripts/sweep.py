@@ -29,9 +29,8 @@ if ntrials:
 sh = _hip.shift_table(cfg.nchan, dms, cfg.start_freq, cfg.bandwidth, cfg.tsamp)
 plans = {}
 for v in variants:
-    os.environ["PU_LDS_BUDGET_KB"] = str(v[1])
-    os.environ["PU_SUB_SHAPE"] = str(v[2] if len(v) > 2 else 0)
-    plans[v] = _hip.Plan(_hip.dtype_code(x.dtype), _hip.PU_ACC_NATIVE, cfg.nchan, cfg.nsamples, sh, group=v[0])
+    plans[v] = _hip.Plan(_hip.dtype_code(x.dtype), _hip.PU_ACC_NATIVE, cfg.nchan, cfg.nsamples, sh, group=v[0],
+                         lds_budget_kb=v[1], shape=v[2] if len(v) > 2 else 0)
     print("variant", v, plans[v].info, flush=True)
 ws = torch.empty(max(p.workspace_bytes for p in plans.values()), dtype=torch.uint8, device=x.device)
 res = {v: [] for v in plans}

@@ -195,6 +195,59 @@ if not have("refmad_in_f64"):
         log("statsmodels 0.12.2 cross-check", meta["refmad_f64_real_statsmodels"],
             float(arrays["refmad_out_f64"]))
 
+
+def real_statsmodels_refmad(a):
+    """ref_mad of ``a`` (float32 or float64) by the real statsmodels 0.12.2 in py3.9: the
+    input's bytes and dtype go through stdin, np.diff runs in that dtype (as in stats.py)."""
+    code = ("import numpy as np,sys;from statsmodels.robust import mad;"
+            f"a=np.frombuffer(sys.stdin.buffer.read(),dtype=np.{a.dtype.name});"
+            "print(repr(float(mad(np.diff(a))/np.sqrt(2))))")
+    r = subprocess.run(["/opt/conda/bin/python3.9", "-W", "ignore", "-c", code], input=a.tobytes(),
+                       capture_output=True, check=True)
+    return float(r.stdout.decode().strip())
+
+
+# ADVICE r3: statsmodels' mad converts its input to float64 (array_like dtype=np.double),
+# so a float32 spectrum's ref_mad is a float64 median of exactly widened float32
+# differences.  Cross-check the float32 input against the real package too, and pin a
+# float32 spectrum whose noisier-channel decision depends on it (with a float32 median /
+# |d - m| the channel at index 100 flips to "noisy").
+if os.path.exists("/opt/conda/bin/python3.9") and not have("refmad_f32_real_statsmodels"):
+    a32 = arrays["refmad_in_f64"].astype(np.float32)
+    meta["refmad_f32_real_statsmodels"] = real_statsmodels_refmad(a32)
+    log("statsmodels 0.12.2 cross-check (float32)", meta["refmad_f32_real_statsmodels"],
+        float(arrays["refmad_out_f32"]))
+if not have("noisy32_spec"):
+    from scipy.signal import medfilt
+    from scipy.stats import norm
+
+    def _mad(a, wide):
+        a = np.asarray(a, dtype=np.double) if wide else np.asarray(a)
+        c = np.median(a) if wide else np.apply_over_axes(np.median, a, 0)
+        return np.median(np.abs(a - c) / norm.ppf(3 / 4.))
+
+    for seed in range(2000):  # first seed where a float32 value separates the two thresholds
+        rng = np.random.default_rng(seed)
+        spec = rng.standard_normal(256).astype(np.float32)
+        spec[100] = 50.0  # the two differences at 100 stay extreme: medians independent of it
+        thr = [medfilt(spec, 7)[100] + 5 * (_mad(np.diff(spec), w) / np.sqrt(2)) for w in (True, False)]
+        lo, hi = min(thr), max(thr)
+        v = np.nextafter(np.float32(lo), np.float32(np.inf))
+        while v <= lo:
+            v = np.nextafter(v, np.float32(np.inf))
+        if v < hi:
+            spec[100] = v
+            break
+    x = np.repeat(spec[:, None], 4, axis=1)  # row means (float32 pairwise sums of 4 equal values) = spec
+    assert np.array_equal(x.mean(1), spec)
+    arrays["noisy32_spec"] = spec
+    arrays["noisy32_mask"] = ref.clean.get_noisier_channels(x)
+    meta["noisy32_seed"] = seed
+    if os.path.exists("/opt/conda/bin/python3.9"):
+        meta["noisy32_refmad_real_statsmodels"] = real_statsmodels_refmad(spec)
+        assert meta["noisy32_refmad_real_statsmodels"] == float(ref.stats.ref_mad(spec))
+    log("noisy32", seed, np.flatnonzero(arrays["noisy32_mask"]))
+
 # ---------------------------------------------------------------- small rebin / roll goldens
 if not have("rebin_in"):
     rng = np.random.default_rng(6)

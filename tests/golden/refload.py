@@ -80,7 +80,7 @@ def _stub_modules():
     robust = types.ModuleType("statsmodels.robust")
 
     def mad(a, c=norm.ppf(3 / 4.), axis=0, center=np.median):
-        a = np.asarray(a)
+        a = np.asarray(a, dtype=np.double)  # array_like(a, "a", ndim=None): dtype=np.double
         if callable(center) and a.size:
             center = np.apply_over_axes(center, a, axis)
         else:

@@ -52,3 +52,25 @@ def test_m0_consumers_checked_on_device_code():
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert " 0 reading" in r.stdout, r.stdout
+
+
+def test_plan_opts_validated_without_gpu():
+    """pu_plan_create_ex checks its options before any HIP call."""
+    from pulsarutils import _hip
+    h = ctypes.c_void_p()
+    sh = (ctypes.c_int64 * 4)()
+    bad = _hip.PlanOpts(group=0, shape=5, lds_budget_kb=0, u8_dma=-1, dt_major=-1)
+    rc = _hip.lib().pu_plan_create_ex(ctypes.byref(h), _hip.PU_F32, 0, 4, 16, ctypes.cast(sh, ctypes.c_void_p), 1,
+                                      ctypes.byref(bad))
+    assert rc == -1 and "shape" in _hip.lib().pu_last_error().decode()
+
+
+def test_production_library_reads_no_tuning_environment():
+    """the tuning knobs (PU_GROUP, PU_SUB_SHAPE, ...) exist only in the
+    diagnostic build; the production library does not even contain their names, so a
+    stray variable in a user's environment cannot change a kernel."""
+    from pulsarutils import _hip
+    blob = open(_hip._LIB_PATH, "rb").read()
+    for knob in (b"PU_SUB_SHAPE", b"PU_GROUP", b"PU_LDS_BUDGET_KB", b"PU_U8_DMA", b"PU_DT_MAJOR", b"PU_CLEAN_BATCH",
+                 b"PU_APPLY_BATCH", b"PU_MEDIAN_GRID", b"PU_COLSEG", b"PU_SUB_SKIP", b"PU_DMA_WAVES"):
+        assert knob not in blob, knob

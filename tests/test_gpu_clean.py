@@ -275,6 +275,22 @@ def test_noisy_channels_device_matches_host(gpu, dt, n):
         np.testing.assert_array_equal(mask, _noisy_host(spec))
 
 
+def test_noisy_channels_float32_mad_golden(gpu, golden):
+    """the float32 spectrum whose mask depends on statsmodels' float64 mad
+    (tests/golden: reference run, mad cross-checked against the real statsmodels 0.12.2):
+    the device decision, through get_noisier_channels on host and device data, equals it."""
+    import torch
+    arrays, _ = golden
+    spec = arrays["noisy32_spec"]
+    mask, flag = _noisy_device(spec)
+    assert flag == 0
+    np.testing.assert_array_equal(mask, arrays["noisy32_mask"])
+    x = np.repeat(spec[:, None], 4, axis=1)
+    np.testing.assert_array_equal(C.get_noisier_channels(x), arrays["noisy32_mask"])
+    got = C.get_noisier_channels(torch.from_numpy(x).cuda())
+    np.testing.assert_array_equal(got.cpu().numpy() if hasattr(got, "cpu") else got, arrays["noisy32_mask"])
+
+
 @pytest.mark.parametrize("bad", [np.nan, np.inf, -np.inf])
 def test_noisy_channels_nonfinite_flag(gpu, bad):
     """A NaN / inf channel mean sets the flag (mask left alone); get_noisier_channels then

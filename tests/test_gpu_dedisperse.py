@@ -102,10 +102,11 @@ def test_dedisperse_random_shapes_exact_f64(gpu, dt, shape):
     np.testing.assert_array_equal(D.dedisperse(x, sh), oracle.dedisperse(x, sh.astype(np.int64)))
 
 
-def _plane(x, shifts, acc, group=0, info=None):
+def _plane(x, shifts, acc, group=0, info=None, **opts):
     t = _hip.require_gpu()
     xd = _hip.to_device(x)
-    plan = _hip.Plan(_hip.dtype_code(xd.dtype), D._acc_code(acc), x.shape[0], x.shape[1], shifts, group=group)
+    plan = _hip.Plan(_hip.dtype_code(xd.dtype), D._acc_code(acc), x.shape[0], x.shape[1], shifts, group=group,
+                     **opts)
     if info is not None:
         info.update(plan.info)
     return plan.dedisperse(xd).cpu().numpy()
@@ -156,7 +157,7 @@ def test_plane_arbitrary_dm_list_large_spread(gpu):
 
 
 @pytest.mark.parametrize("dt", ["u8", "f32", "f64"])
-def test_plane_subband_small_lds_budget(gpu, dt, monkeypatch):
+def test_plane_subband_small_lds_budget(gpu, dt):
     """A small LDS budget: one group per stage, short DM tiles, many stages per tile."""
     c = CONFIGS["C5"]
     rng = np.random.default_rng(21)
@@ -165,9 +166,8 @@ def test_plane_subband_small_lds_budget(gpu, dt, monkeypatch):
     x = {"u8": x.astype(np.uint8), "f32": x.astype(np.float32), "f64": x}[dt]
     dms = np.linspace(c.dmmin, c.dmmax, 90)
     sh = _hip.shift_table(c.nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
-    monkeypatch.setenv("PU_LDS_BUDGET_KB", "96")
     info = {}
-    plane = _plane(x, sh, "f32" if dt == "f64" else "native", 4, info)
+    plane = _plane(x, sh, "f32" if dt == "f64" else "native", 4, info, lds_budget_kb=96)
     assert info["group"] == 4 and info["stages"] > 2 * info["dm_tiles"], info
     for k in range(0, 90, 7):
         ref = oracle.dedisperse(x, sh[k])
@@ -180,8 +180,8 @@ def test_plane_subband_small_lds_budget(gpu, dt, monkeypatch):
 @pytest.mark.parametrize("group", [4, 8])
 @pytest.mark.parametrize("shape", ["1", "2"])
 @pytest.mark.parametrize("dt", ["u8", "f32"])
-def test_plane_subband_pair_shape(gpu, dt, shape, group, monkeypatch):
-    """The time-tile-256 subband shapes (PU_SUB_SHAPE=1 pair: 8 waves x 16 trials, two
+def test_plane_subband_pair_shape(gpu, dt, shape, group):
+    """The time-tile-256 subband shapes (shape 1 pair: 8 waves x 16 trials, two
     workgroups per CU; 2 tall: 16 waves x 16 trials) against the oracle, ragged N and a
     partial last group (nchan % G != 0 for G = 4 and 8)."""
     c = CONFIGS["C2"]
@@ -191,9 +191,8 @@ def test_plane_subband_pair_shape(gpu, dt, shape, group, monkeypatch):
     x = x.astype(np.uint8) if dt == "u8" else x.astype(np.float32)
     dms = np.linspace(0.0, 60.0, 150)
     sh = _hip.shift_table(nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
-    monkeypatch.setenv("PU_SUB_SHAPE", shape)
     info = {}
-    plane = _plane(x, sh, "native", group, info)
+    plane = _plane(x, sh, "native", group, info, shape=int(shape))
     assert info["group"] == group and info["time_tile"] == 256, info
     for k in range(0, 150, 11):
         ref = oracle.dedisperse(x, sh[k])
@@ -293,15 +292,15 @@ def test_search_c1_float32_accumulation(gpu, golden, acc):
 
 @pytest.mark.parametrize("group", ["1", "4"])
 @pytest.mark.parametrize("dt", ["f32", "u8"])
-def test_search_ragged_small(gpu, dt, group, monkeypatch):
+def test_search_ragged_small(gpu, dt, group):
     """Tiny / ragged inputs: N smaller than a time tile, odd nchan, N % 8 != 0."""
-    monkeypatch.setenv("PU_GROUP", group)
     rng = np.random.default_rng(3)
     for nchan, n in [(3, 37), (5, 200), (31, 1001), (130, 3000)]:
         x = rng.random((nchan, n)) * 10
         x = x.astype(np.float32) if dt == "f32" else x.astype(np.uint8)
         dms = np.linspace(0, 300, 23)
-        g = D._dedispersion_search(x, dms, nchan, 400., 100., 1e-3)
+        with D.planner_options(group=int(group)):
+            g = D._dedispersion_search(x, dms, nchan, 400., 100., 1e-3)
         o = oracle.search(x, dms, 400., 100., 1e-3)
         for a, b in zip(g[:3], o[:3]):
             np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-9)
@@ -377,7 +376,7 @@ def test_default_group_cost_model(gpu, golden, name, group, tile):
         assert np.all(np.abs(rows[k] - ref) <= f32_bound(x, sh[i])), i
 
 
-def test_plan_cache_reuse(gpu, monkeypatch):
+def test_plan_cache_reuse(gpu):
     """Repeated numpy-API calls reuse the cached plan (same results); a different trial
     grid or planner variable builds a new one."""
     c = CONFIGS["C2"]
@@ -394,11 +393,13 @@ def test_plan_cache_reuse(gpu, monkeypatch):
         np.testing.assert_array_equal(u, v)
     _, p3 = D.search_device(x, dms[:-1], *args)
     assert p3 is not p1
-    monkeypatch.setenv("PU_SUB_SHAPE", "1")
-    _, p4 = D.search_device(x, dms, *args)
-    assert p4 is not p1
-    for u, v in zip(a, D._dedispersion_search(x, dms, *args)):
-        np.testing.assert_allclose(u, v, rtol=1e-5)
+    with D.planner_options(shape=1):
+        _, p4 = D.search_device(x, dms, *args)
+        assert p4 is not p1 and p4.info["time_tile"] == 256
+        for u, v in zip(a, D._dedispersion_search(x, dms, *args)):
+            np.testing.assert_allclose(u, v, rtol=1e-5)
+    _, p5 = D.search_device(x, dms, *args)  # the scope ended: the default plan again
+    assert p5 is p1
 
 
 def test_search_c3_full_size_u8(gpu):
@@ -458,9 +459,9 @@ def test_search_u8_bitexact_series_c3_slice(gpu):
 
 @pytest.mark.parametrize("group", [4, 8])
 @pytest.mark.parametrize("shape", ["0", "1", "2"])
-def test_plane_u8_dma_rows(gpu, shape, group, monkeypatch):
+def test_plane_u8_dma_rows(gpu, shape, group):
     """8-bit rows staged by LDS-DMA (N % 4 == 0): bit-exact against the oracle and the
-    global-read build (PU_U8_DMA=0), with a partial last group (130 % G != 0), row
+    global-read build (u8_dma=False), with a partial last group (130 % G != 0), row
     misalignments (base % 4 != 0), a padded row stride and a view whose rows are not
     4-byte aligned."""
     import torch
@@ -470,17 +471,15 @@ def test_plane_u8_dma_rows(gpu, shape, group, monkeypatch):
     x = (rng.random((nchan, n)) * 60).astype(np.uint8)
     dms = np.linspace(0.0, 60.0, 150)
     sh = _hip.shift_table(nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
-    monkeypatch.setenv("PU_SUB_SHAPE", shape)
-    plan = _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, nchan, n, sh, group=group)
+    plan = _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, nchan, n, sh, group=group, shape=int(shape))
     assert plan.info["group"] == group, plan.info
     xd = _hip.to_device(x)
     plane = plan.dedisperse(xd).cpu().numpy()
     for k in range(0, 150, 13):
         np.testing.assert_array_equal(plane[k].astype(np.float64), oracle.dedisperse(x, sh[k]))
-    monkeypatch.setenv("PU_U8_DMA", "0")
-    ref = _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, nchan, n, sh, group=group).dedisperse(xd).cpu().numpy()
+    ref = _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, nchan, n, sh, group=group, shape=int(shape),
+                    u8_dma=False).dedisperse(xd).cpu().numpy()
     np.testing.assert_array_equal(plane, ref)
-    monkeypatch.delenv("PU_U8_DMA")
     big = torch.zeros((nchan, n + 8), dtype=torch.uint8, device=xd.device)
     big[:, 4:4 + n] = xd
     np.testing.assert_array_equal(plan.dedisperse(big[:, 4:4 + n]).cpu().numpy(), plane)  # ld = n + 8

@@ -1,0 +1,48 @@
+"""the multi-rank HIP path on the one leased GPU, before any 8-GPU run
+depends on it.  2 and 3 ranks (processes) share cuda:0 over a ``gloo`` process group
+(RCCL refuses two ranks per device) and run the product path's world > 1 branch for
+real: chunked broadcast from a non-zero source on the communication stream, staging
+pack / unpack, event-gated time-tile launches (pu_plan_search_tiles) on the compute
+stream, pu_plan_finalize, and sharded_search's all_gather - each rank's outputs equal
+the single-rank search bit for bit (tests/mr_worker.py).  The reference's parallelism
+is the prange over trials (dedispersion.py:174-181)."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world,case", [(2, "C5"), (3, "C5"), (2, "C3s"), (3, "C3s"), (2, "C5m")])
+def test_multirank_pipelined_and_sharded_on_one_gpu(gpu, world, case):
+    port = _free_port()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="4")
+    procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "mr_worker.py"), str(r), str(world), str(port),
+                               case], stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env)
+             for r in range(world)]
+    outs = []
+    try:
+        for p in procs:
+            o, e = p.communicate(timeout=240)
+            outs.append((p.returncode, o.decode(errors="replace"), e.decode(errors="replace")))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    for r, (rc, o, e) in enumerate(outs):
+        assert rc == 0 and f"RANK {r} OK" in o, f"rank {r} rc {rc}\n{o}\n{e[-4000:]}"
+    print("\n".join(o.strip() for _, o, _ in outs))

@@ -126,3 +126,51 @@ def test_ready_tiles_read_only_landed_columns(gpu, dt, offset):
     got = [o.cpu().numpy() for o in plan.finalize(ws, x)]
     for a, b in zip(full, got):
         np.testing.assert_array_equal(a, b)
+
+
+def test_cached_plan_two_threads(gpu):
+    """one cached plan searched from two threads at once (ctypes releases the
+    GIL), each thread on its own stream; one input is constant, so every one of its trials
+    is certified by the exact recheck (resolve_flagged: the pinned CertState read-back and
+    the recheck scratch), the other is noise.  Every result equals the single-threaded
+    one: the library's per-plan lock keeps the calls' certification state apart."""
+    import threading
+
+    import torch
+    c = CONFIGS["C5"]
+    rng = np.random.default_rng(9)
+    n = 1 << 15
+    noise = torch.from_numpy((rng.random((c.nchan, n)) * 50).astype(np.uint8)).cuda()
+    const = torch.full((c.nchan, n), 7, dtype=torch.uint8, device=noise.device)
+    dms = np.linspace(c.dmmin, c.dmmax, 120)
+    args = (c.nchan, c.start_freq, c.bandwidth, c.tsamp)
+    want = {}
+    for name, x in (("noise", noise), ("const", const)):
+        (o, plan) = D.search_device(x, dms, *args)
+        want[name] = [t.cpu().numpy() for t in o]
+        if name == "const":
+            assert plan.cert_info()["rechecked"] == dms.size
+    _, p1 = D.search_device(noise, dms, *args)
+    _, p2 = D.search_device(const, dms, *args)
+    assert p1 is p2  # one cached plan serves both inputs
+    errors = []
+
+    def worker(name, x):
+        try:
+            s = torch.cuda.Stream(device=x.device)
+            with torch.cuda.stream(s):
+                for _ in range(6):
+                    o, _ = D.search_device(x, dms, *args)
+                    got = [t.cpu().numpy() for t in o]
+                    for a, b in zip(want[name], got):
+                        np.testing.assert_array_equal(a, b)
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append(f"{name}: {e!r}")
+
+    th = [threading.Thread(target=worker, args=a) for a in (("noise", noise), ("const", const))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th), "thread hung"
+    assert not errors, errors

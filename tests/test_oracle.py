@@ -113,6 +113,24 @@ def test_mad_matches_statsmodels(golden):
     assert co.ref_mad(a.astype(np.float32)) == arrays["refmad_out_f32"]
     if "refmad_f64_real_statsmodels" in meta:
         assert float(co.ref_mad(a)) == meta["refmad_f64_real_statsmodels"]
+    # float32 input: statsmodels widens it to float64, cross-checked against the
+    # real package in /opt/conda/bin/python3.9 by make_golden.py
+    assert float(co.ref_mad(a.astype(np.float32))) == meta["refmad_f32_real_statsmodels"]
+
+
+def test_noisier_channels_float32_mad_dtype(golden):
+    """A float32 spectrum whose mask depends on the mad's dtype (make_golden.py, seed in
+    the meta): the reference (statsmodels' float64 mad, cross-checked against the real
+    package) keeps channel 100; a float32 median / |d - m| would flag it."""
+    from scipy.signal import medfilt
+    arrays, meta = golden
+    spec = arrays["noisy32_spec"]
+    x = np.repeat(spec[:, None], 4, axis=1)
+    np.testing.assert_array_equal(co.noisier_channels(x), arrays["noisy32_mask"])
+    assert float(co.ref_mad(spec)) == meta["noisy32_refmad_real_statsmodels"]
+    d = np.diff(spec)  # the float32-median variant flips the decision
+    m32 = np.median(np.abs(d - np.apply_over_axes(np.median, d, 0)) / co.MAD_C) / np.sqrt(2)
+    assert (spec > medfilt(spec, 7) + 5 * m32)[100] and not arrays["noisy32_mask"][100]
 
 
 def _check_clean(arrays, meta, tag, x):
