@@ -178,6 +178,44 @@ def clean_bench(dev, steps):
     return res
 
 
+def acc_f64_bench(x, dms, cfg, steps):
+    """The reference-precision search on the headline workload: the same C2 filterbank and
+    trials with float64 accumulation in channel order (dedisp_kernel; the series of every
+    trial is the reference's dedisperse() bit for bit, dedispersion.py:86-98), as the
+    drop-in's dedisperse / show=True / search_by_chunks defaults run it.  Roofline: the
+    float64 vector-add peak, and the LDS array (window reads + staged rows)."""
+    sh = _hip.shift_table(cfg.nchan, dms, cfg.start_freq, cfg.bandwidth, cfg.tsamp)
+    plan = _hip.Plan(_hip.dtype_code(x.dtype), _hip.PU_ACC_F64, cfg.nchan, cfg.nsamples, sh)
+    ws = torch.empty(plan.workspace_bytes, dtype=torch.uint8, device=x.device)
+    outs = plan._outs_ws(x.device, None, ws)[0]
+    plan.search(x, out=outs, workspace=ws)  # warm-up
+    torch.cuda.synchronize()
+    plan.enable_timing(steps)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        plan.search(x, out=outs, workspace=ws)
+    torch.cuda.synchronize()
+    step_ms = (time.perf_counter() - t0) / steps * 1e3
+    kms = float(np.mean(plan.kernel_times_ms(steps)))
+    adds = float(cfg.nchan) * cfg.nsamples * dms.size
+    info = plan.info
+    lds = info["lds_traffic"] / (kms / 1e3) / 1e12
+    res = {"workload": f"{cfg.name} ({dms.size} trials), float64 accumulation in channel order (acc='f64')",
+           "kernel": "dedisp_kernel", "steps": steps, "ms_per_step": round(step_ms, 4), "kernel_ms": round(kms, 4),
+           "value": dms.size * cfg.nsamples / (step_ms / 1e3), "unit": "DM-trial samples/s",
+           "roofline": {"bound": "valu", "achieved": round(adds / (kms / 1e3) / 1e12, 3),
+                        "peak": VALU_F64_ADD_PEAK_TFLOPS, "unit": "TFLOP/s (f64 adds)",
+                        "frac": round(adds / (kms / 1e3) / 1e12 / VALU_F64_ADD_PEAK_TFLOPS, 4),
+                        "lds_bytes_per_launch": info["lds_traffic"], "lds_achieved_TBps": round(lds, 2),
+                        "lds_peak_TBps": LDS_PEAK_TBPS, "lds_frac": round(lds / LDS_PEAK_TBPS, 4)},
+           "plan": {k: info[k] for k in ("dm_tiles", "time_tiles", "trials_per_tile", "time_tile", "chans_per_step",
+                                         "lds_bytes")},
+           "best_dm": float(dms[int(torch.argmax(outs[2]).item())]), "certify": plan.cert_info()}
+    del plan, ws, outs
+    torch.cuda.empty_cache()
+    return res
+
+
 def c3_strong(dev, world, rank, steps, chunks):
     """configs[2] as BASELINE states it: the C3 filterbank (4096 chan x 2^22 uint8, 17.2 GB)
     with its 5000 DM trials split contiguously over the N ranks (strong scaling).
@@ -268,6 +306,9 @@ def main():
     ap.add_argument("--no-c3-strong", action="store_true",
                     help="skip the configs[2] sub-benchmark (C3: 5000 trials split over the N GPUs)")
     ap.add_argument("--c3-steps", type=int, default=2)
+    ap.add_argument("--no-acc-f64", action="store_true",
+                    help="skip the float64-accumulation (reference precision) sub-benchmark")
+    ap.add_argument("--acc-f64-steps", type=int, default=3)
     ap.add_argument("--allow-knobs", action="store_true",
                     help="time even with PU_* / PULSARUTILS_* tuning variables set (sweeps only: the line "
                          "is marked invalid)")
@@ -431,7 +472,16 @@ def main():
                          "executed_tflops": round(info["exec_adds"] / (kernel_ms / 1e3) / 1e12, 3),
                          "lds_bytes_per_launch": info["lds_traffic"], "lds_achieved_TBps": round(lds, 2),
                          "lds_peak_TBps": LDS_PEAK_TBPS, "lds_frac": round(lds / LDS_PEAK_TBPS, 4),
-                         "group": info["group"]})
+                         "group": info["group"], "binding": "lds",
+                         "binding_note": "frac is SURVEY 8(d)'s brute-force-equivalent adds / the f32 VALU-add "
+                                         "peak; the subband decomposition executes group x fewer adds, and the "
+                                         "unit that binds it is the LDS array: lds_frac"})
+
+    f64 = None
+    if rank == 0 and world == 1 and not args.no_acc_f64 and args.acc == "native" and cfg.dtype != "f64":
+        log("acc_f64 ...")
+        f64 = acc_f64_bench(x, dms, cfg, args.acc_f64_steps)
+        log(f"acc_f64 kernel {f64['kernel_ms']:.3f} ms, step {f64['ms_per_step']:.3f} ms")
 
     clean = None
     if rank == 0 and world == 1 and not args.no_clean:
@@ -475,6 +525,8 @@ def main():
                 "certify": dict(cert, what="trials of the last timed step whose fast statistics could not be "
                                            "certified and were recomputed exactly (DESIGN.md §4.5)"),
                 "env": knobs, "valid": not knobs}
+        if f64 is not None:
+            line["acc_f64"] = f64
         if c3 is not None:
             line["c3_strong"] = c3
         if bcast is not None:

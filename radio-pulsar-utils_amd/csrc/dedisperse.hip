@@ -95,40 +95,47 @@ __device__ __forceinline__ uint64_t stamp()
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
-// In-place K-sample window read: 4 x ds_read_b64 at 512-byte strides + wait.  One asm
-// block that overwrites the window registers, so the register allocator never keeps
-// two versions alive.  Outputs are early-clobber: an LDS read can return (and write
-// its destination) before the block's later reads have consumed the address VGPR.
-__device__ __forceinline__ void read_window(double (&w)[4], uint32_t addr)
-{
-    asm volatile(
-        "ds_read_b64 %0, %4\n\t"
-        "ds_read_b64 %1, %4 offset:512\n\t"
-        "ds_read_b64 %2, %4 offset:1024\n\t"
-        "ds_read_b64 %3, %4 offset:1536\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3])
-        : "v"(addr)
-        : "memory");
-}
-
-// Same reads without the wait (prefetch of the next channel's first window); the
-// registers are only consumed after wait_window() on them.
+// Channel-mode window reads: J x ds_read_b64 at 512-byte strides (inline asm: hipcc
+// would merge pairs into ds_read2st64_b64, which runs at half the LDS rate).  Outputs are
+// early-clobber: an LDS read can return (and write its destination) before the block's
+// later reads have consumed the address VGPR.  prefetch_window issues without a wait; the
+// registers are consumed only after wait_window() on them (a counted-free lgkmcnt(0)
+// that "defines" them, so no use can be hoisted above it).
+template <int J>
 __device__ __forceinline__ void prefetch_window(double (&w)[4], uint32_t addr)
 {
-    asm volatile(
-        "ds_read_b64 %0, %4\n\t"
-        "ds_read_b64 %1, %4 offset:512\n\t"
-        "ds_read_b64 %2, %4 offset:1024\n\t"
-        "ds_read_b64 %3, %4 offset:1536"
-        : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3])
-        : "v"(addr)
-        : "memory");
+    if constexpr (J == 4)
+        asm volatile(
+            "ds_read_b64 %0, %4\n\t"
+            "ds_read_b64 %1, %4 offset:512\n\t"
+            "ds_read_b64 %2, %4 offset:1024\n\t"
+            "ds_read_b64 %3, %4 offset:1536"
+            : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3])
+            : "v"(addr)
+            : "memory");
+    else
+        asm volatile(
+            "ds_read_b64 %0, %2\n\t"
+            "ds_read_b64 %1, %2 offset:512"
+            : "=&v"(w[0]), "=&v"(w[1])
+            : "v"(addr)
+            : "memory");
 }
 
+template <int J>
 __device__ __forceinline__ void wait_window(double (&w)[4])
 {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]) : : "memory");
+    if constexpr (J == 4)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]) : : "memory");
+    else
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w[0]), "+v"(w[1]) : : "memory");
+}
+
+template <int J>
+__device__ __forceinline__ void read_window(double (&w)[4], uint32_t addr)
+{
+    prefetch_window<J>(w, addr);
+    wait_window<J>(w);
 }
 
 // Empty asm that "uses" one trial's accumulators: keeps each trial's adds ahead of the
@@ -157,19 +164,30 @@ __device__ __forceinline__ Tl window_elem(const double (&w)[4], int k)
     }
 }
 
-// Add one channel's contribution to all D trials of this wave.  ``rec`` = 8 u16
-// window records (byte offset | reload flag << 15); ``w`` holds trial 0's window.
-template <typename Tl, typename Ta, int K>
+// Add one channel's contribution to all D trials of this wave.  ``rec`` = 8 u16 window
+// records (byte offset | reload flag << 15); ``w`` holds trial 0's window (raw LDS
+// elements).  The window's K samples are taken into the accumulation type once per
+// window (``wv``: a float32 -> float64 conversion per changed window, not per trial and
+// sample: round 3 converted on every add, two VALU ops per float64 add at C2 acc='f64');
+// a trial whose window differs from the previous trial's re-reads it in place.
+template <typename Tl, typename Ta, int K, int J>
 __device__ __forceinline__ void channel_trials(Ta (&acc)[kD][K], double (&w)[4], const u32x4 rec, uint32_t cbase)
 {
+    Ta wv[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) wv[k] = static_cast<Ta>(window_elem<Tl>(w, k));
 #pragma unroll
     for (int d = 0; d < kD; ++d) {
         if (d > 0) {
             const uint32_t word = rec[d >> 1] >> (16 * (d & 1));
-            if (word & 0x8000u) read_window(w, cbase + (word & 0x7fffu));
+            if (word & 0x8000u) {
+                read_window<J>(w, cbase + (word & 0x7fffu));
+#pragma unroll
+                for (int k = 0; k < K; ++k) wv[k] = static_cast<Ta>(window_elem<Tl>(w, k));
+            }
         }
 #pragma unroll
-        for (int k = 0; k < K; ++k) acc[d][k] += static_cast<Ta>(window_elem<Tl>(w, k));
+        for (int k = 0; k < K; ++k) acc[d][k] += wv[k];
         pin_accumulators(acc[d]);
     }
 }
@@ -372,7 +390,7 @@ __device__ __forceinline__ void stats_full_pairs(const f32x2 (&acc)[D][J], const
 {
     static_assert(D % 8 == 0, "trials per wave");
     constexpr int NV = 9;  // per trial: sum y, sum of squares w = 1,2,4,8, max w = 1,2,4,8
-    const bool even = (lane & 1) == 0, quad = (lane & 3) == 0;
+    const bool even = (lane & 1) == 0;
     // The shift (recorded as the partial's center): the tile mean of the wave's first
     // trial.  The wave's D trials are a few DM steps apart, so their tile means differ by
     // a small fraction of the std: the shifted squares stay near the variance and their
@@ -389,28 +407,41 @@ __device__ __forceinline__ void stats_full_pairs(const f32x2 (&acc)[D][J], const
     }
     const f32x2 k1 = {kt, kt};
     const float k2 = 2.0f * kt, k4 = 4.0f * kt, k8 = 8.0f * kt;
+    static_assert(J % 2 == 0, "sample pairs are taken two blocks at a time");
+    const bool lo2 = (lane & 2) == 0;
     auto lane_stats = [&](int d, float (&v)[NV]) {
         f32x2 s1 = {0.0f, 0.0f}, q1 = s1;
         float q2 = 0.0f, q4 = 0.0f, q8 = 0.0f;
         float m1 = -INFINITY, m2 = -INFINITY, m4 = -INFINITY, m8 = -INFINITY;
 #pragma unroll
-        for (int j = 0; j < J; ++j) {
-            const f32x2 x = acc[d][j];
-            const f32x2 y = x - k1;
-            s1 += y;
-            q1 = __builtin_elementwise_fma(y, y, q1);
-            m1 = vmax3(m1, x.x, x.y);
-            const float r2 = x.x + x.y;                 // width 2 (every lane)
-            const float y2 = r2 - k2;
-            q2 = __builtin_fmaf(y2, y2, q2);
-            m2 = vmax(m2, r2);
-            // widths 4 and 8 on every lane; only even lanes (4) / lanes 4k (8) hold aligned
-            // windows, so the others' sums and maxima are dropped once, after the loop
-            const float r4 = r2 + row_down<1>(r2);
+        for (int j = 0; j < J; j += 2) {
+            float r2[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const f32x2 x = acc[d][j + h];
+                const f32x2 y = x - k1;
+                s1 += y;
+                q1 = __builtin_elementwise_fma(y, y, q1);
+                m1 = vmax3(m1, x.x, x.y);
+                r2[h] = x.x + x.y;  // width 2 (every lane)
+                const float y2 = r2[h] - k2;
+                q2 = __builtin_fmaf(y2, y2, q2);
+                m2 = vmax(m2, r2[h]);
+            }
+            // widths 4 and 8 of the two blocks j, j + 1 packed into one register (every
+            // lane useful, round 4): even lanes hold block j's width-4 sums (r2 of lanes l,
+            // l + 1), odd lanes block j + 1's (lanes l - 1, l) - one quad_perm [1,0,3,2] add
+            // of the parity-swapped r2; then quad_perm [2,3,0,1] pairs them into width 8 on
+            // lanes 4k (block j) and 4k + 1 (block j + 1), the other two lanes of each quad
+            // holding copies (dropped after the loop).  (Round 3: both widths on every lane
+            // of every block, half / three quarters of them dropped.)
+            const float a4 = even ? r2[0] : r2[1];
+            const float c4 = even ? r2[1] : r2[0];
+            const float r4 = a4 + dpp<0xB1>(0.0f, c4);
             const float y4 = r4 - k4;
             q4 = __builtin_fmaf(y4, y4, q4);
             m4 = vmax(m4, r4);
-            const float r8 = r4 + row_down<2>(r4);
+            const float r8 = r4 + dpp<0x4E>(0.0f, r4);
             const float y8 = r8 - k8;
             q8 = __builtin_fmaf(y8, y8, q8);
             m8 = vmax(m8, r8);
@@ -418,12 +449,12 @@ __device__ __forceinline__ void stats_full_pairs(const f32x2 (&acc)[D][J], const
         v[0] = s1.x + s1.y;
         v[1] = q1.x + q1.y;
         v[2] = q2;
-        v[3] = even ? q4 : 0.0f;
-        v[4] = quad ? q8 : 0.0f;
+        v[3] = q4;
+        v[4] = lo2 ? q8 : 0.0f;
         v[5] = m1;
         v[6] = m2;
-        v[7] = even ? m4 : -INFINITY;
-        v[8] = quad ? m8 : -INFINITY;
+        v[7] = m4;
+        v[8] = lo2 ? m8 : -INFINITY;
     };
     auto add = [](float x, float y) { return x + y; };
     auto mx = [](float x, float y) { return vmax(x, y); };
@@ -466,6 +497,169 @@ __device__ __forceinline__ void stats_full_pairs(const f32x2 (&acc)[D][J], const
             if (f < 13 && slot0 + trial < cnt)
                 reinterpret_cast<float *>(a.partials)[((size_t)(first + slot0 + trial) * a.ntt + tt) * kPartStride + f] = v;
         }
+    }
+}
+
+// float64 counterparts of the permlane combines (two swaps per value, one per dword)
+__device__ __forceinline__ double vmax_f64(double a, double b)
+{
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));  // IEEE mode: skips a NaN operand
+    return r;
+}
+__device__ __forceinline__ double f64_of(unsigned lo, unsigned hi)
+{
+    return __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
+}
+template <class Op>
+__device__ __forceinline__ double swap32_combine_f64(double a, double b, Op op)
+{
+    const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)ua, (unsigned)ub, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+    return op(f64_of((unsigned)lo[0], (unsigned)hi[0]), f64_of((unsigned)lo[1], (unsigned)hi[1]));
+}
+template <class Op>
+__device__ __forceinline__ double swap16_combine_f64(double a, double b, Op op)
+{
+    const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)ua, (unsigned)ub, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+    return op(f64_of((unsigned)lo[0], (unsigned)hi[0]), f64_of((unsigned)lo[1], (unsigned)hi[1]));
+}
+
+// Search-mode outputs of a channel-mode wave with float64 accumulators (the reference-
+// precision search, acc='f64') for a FULL time tile: the partial record of write_outputs
+// (kt | max, sum, sum of squares of the 1/2/4/8-sample rebinned series), computed as
+// stats_full_pairs does for float32 - per-lane statistics without bounds tests, widths 2/4/8
+// by DPP row shifts accumulated on every lane and the misaligned lanes dropped once, and the
+// wave reductions of the 8 trials together on the permlane32/16 swaps, lane 16 r + f
+// storing field f of row r's trial.  Round 3 reduced every statistic of every trial with
+// its own 6-step DPP chain (about 480 instructions per trial: the larger part of the C1
+// kernel).  All sums in float64 (<= 11 roundings per term: gamma = 2^-44 holds).
+// E = 1: lane l owns samples t0 + l + 64 k; E = 2: pairs t0 + 2 l + 128 j + {0, 1}.
+template <int E, int K>
+__device__ __forceinline__ void stats_full_f64(const double (&acc)[kD][K], const DedispArgs &a, int first, int slot0,
+                                               int cnt, int tt, int lane)
+{
+    constexpr int D = kD;
+    constexpr int NV = 9;  // sum y, sum of squares w = 1, 2, 4, 8, max w = 1, 2, 4, 8
+    static_assert(D == 8, "8 trials per wave");
+    double kt;  // the tile mean of the wave's first trial (the shift of every record)
+    {
+        double s0 = acc[0][0];
+#pragma unroll
+        for (int k = 1; k < K; ++k) s0 += acc[0][k];
+        const uint64_t b = __builtin_bit_cast(uint64_t, wave_sum_to63(s0));
+        kt = f64_of((unsigned)__builtin_amdgcn_readlane((int)(uint32_t)b, 63),
+                    (unsigned)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), 63)) *
+             (1.0 / (64.0 * K));
+    }
+    const double k2 = 2.0 * kt, k4 = 4.0 * kt, k8 = 8.0 * kt;
+    const bool m2ok = E == 2 || (lane & 1) == 0;                 // aligned width-2 windows
+    const bool m4ok = E == 2 ? (lane & 1) == 0 : (lane & 3) == 0;
+    const bool m8ok = E == 2 ? (lane & 3) == 0 : (lane & 7) == 0;
+    auto lane_stats = [&](int d, double (&v)[NV]) {
+        double s1 = 0.0, q1 = 0.0, q2 = 0.0, q4 = 0.0, q8 = 0.0;
+        double m1 = -INFINITY, m2 = -INFINITY, m4 = -INFINITY, m8 = -INFINITY;
+        auto w1 = [&](double x) {
+            const double y = x - kt;
+            s1 += y;
+            q1 = __builtin_fma(y, y, q1);
+            m1 = vmax_f64(m1, x);
+        };
+        auto wn = [&](double r, double k, double &q, double &m) {
+            const double y = r - k;
+            q = __builtin_fma(y, y, q);
+            m = vmax_f64(m, r);
+        };
+        if constexpr (E == 1) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const double x = acc[d][k];
+                w1(x);
+                const double r2 = x + dpp_undef<0x101>(x);  // row_shl:1, zero past the row
+                wn(r2, k2, q2, m2);
+                const double r4 = r2 + dpp_undef<0x102>(r2);
+                wn(r4, k4, q4, m4);
+                const double r8 = r4 + dpp_undef<0x104>(r4);
+                wn(r8, k8, q8, m8);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < K / 2; ++j) {
+                const double x0 = acc[d][2 * j], x1 = acc[d][2 * j + 1];
+                w1(x0);
+                w1(x1);
+                const double r2 = x0 + x1;
+                wn(r2, k2, q2, m2);
+                const double r4 = r2 + dpp_undef<0x101>(r2);
+                wn(r4, k4, q4, m4);
+                const double r8 = r4 + dpp_undef<0x102>(r4);
+                wn(r8, k8, q8, m8);
+            }
+        }
+        v[0] = s1;
+        v[1] = q1;
+        v[2] = m2ok ? q2 : 0.0;
+        v[3] = m4ok ? q4 : 0.0;
+        v[4] = m8ok ? q8 : 0.0;
+        v[5] = m1;
+        v[6] = m2ok ? m2 : -INFINITY;
+        v[7] = m4ok ? m4 : -INFINITY;
+        v[8] = m8ok ? m8 : -INFINITY;
+    };
+    auto add = [](double x, double y) { return x + y; };
+    auto mx = [](double x, double y) { return vmax_f64(x, y); };
+    auto row_all = [&](double v, bool is_max) {
+        if (is_max) {
+            v = vmax_f64(v, dpp_undef<0xB1>(v));
+            v = vmax_f64(v, dpp_undef<0x4E>(v));
+            v = vmax_f64(v, dpp_undef<0x124>(v));
+            return vmax_f64(v, dpp_undef<0x128>(v));
+        }
+        v += dpp_undef<0xB1>(v);
+        v += dpp_undef<0x4E>(v);
+        v += dpp_undef<0x124>(v);
+        return v + dpp_undef<0x128>(v);
+    };
+    // Trials in pairs (k, k + 4): swap32 -> every value holds trial k in lanes 0-31 and
+    // k + 4 in lanes 32-63; then swap16 pairs two VALUES of the pair ((s1, q1), (q2, q4),
+    // (q8, q8), (m1, m2), (m4, m8)): rows 0 / 1 hold the first / second value for trial k,
+    // rows 2 / 3 for trial k + 4, and 4 fused row steps give every lane its row's total.
+    // Lane 16 r + f stores field f of its row's trial when that row holds the field's value
+    // (one store instruction per pair).  One pair at a time (scheduling barriers between
+    // them), so the accumulators die as the partials are made: <= 128 VGPRs, 4 waves per
+    // SIMD (8 trials at once, as stats_full_pairs does for float32, took 158-178).
+    const int li = lane & 15, row = lane >> 4, rp = row & 1;
+    const bool st_lane = rp == 0 ? (li <= 2 || li == 5 || li == 6 || li == 7 || li == 8 || li == 11 || li == 12)
+                                 : (li == 3 || li == 4 || li == 9 || li == 10);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        double va[NV], vb[NV];
+        lane_stats(k, va);
+        __builtin_amdgcn_sched_barrier(0);
+        lane_stats(k + 4, vb);
+        double U[NV];
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+            U[i] = i < 5 ? swap32_combine_f64(va[i], vb[i], add) : swap32_combine_f64(va[i], vb[i], mx);
+        const double P0 = row_all(swap16_combine_f64(U[0], U[1], add), false);  // s1 | q1
+        const double P1 = row_all(swap16_combine_f64(U[2], U[3], add), false);  // q2 | q4
+        const double P2 = row_all(swap16_combine_f64(U[4], U[4], add), false);  // q8 | q8
+        const double P3 = row_all(swap16_combine_f64(U[5], U[6], mx), true);    // m1 | m2
+        const double P4 = row_all(swap16_combine_f64(U[7], U[8], mx), true);    // m4 | m8
+        // field li: 0 kt, 1 + 3 w + {0 max, 1 sum, 2 sum of squares} for width index w
+        double v = kt;
+        v = (li == 1 || li == 4) ? P3 : v;
+        v = (li == 2 || li == 3 || li == 5 || li == 8 || li == 11) ? P0 : v;
+        v = (li == 6 || li == 9) ? P1 : v;
+        v = (li == 7 || li == 10) ? P4 : v;
+        v = li == 12 ? P2 : v;
+        const int trial = row < 2 ? k : k + 4;
+        if (st_lane && slot0 + trial < cnt)
+            reinterpret_cast<double *>(a.partials)[((size_t)(first + slot0 + trial) * a.ntt + tt) * kPartStride + li] = v;
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -575,7 +769,9 @@ __device__ __forceinline__ void write_outputs(const Ta (&acc)[D][K], const Dedis
 }
 
 template <typename Tin, typename Tl, typename Ta, bool PLANE, bool STATS>
-__global__ void __launch_bounds__(kThreads)
+// 4 waves per SIMD (2 workgroups per CU): <= 128 VGPRs, enforced (the float64 epilogue
+// left alone took 130, i.e. 3 waves per SIMD)
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
 dedisp_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const int32_t *__restrict__ tile_count,
               const int32_t *__restrict__ tile_rowlen, const int32_t *__restrict__ base_tab,
               const u32x4 *__restrict__ rec_tab)
@@ -584,7 +780,9 @@ dedisp_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const int32_
     constexpr bool kDma = std::is_same<Tin, Tl>::value;
     constexpr int SZ = (int)sizeof(Tl);
     constexpr int E = 8 / SZ;     // samples per 8-byte LDS read
-    constexpr int J = 4;          // reads per window
+    // reads per window: 4, or 2 when float32 rows feed float64 accumulators (8 trials x 8
+    // float64 samples per lane would take 164 VGPRs: 3 waves per SIMD)
+    constexpr int J = (sizeof(Ta) == 8 && sizeof(Tl) == 4) ? 2 : 4;
     constexpr int K = E * J;      // samples per lane
     constexpr int TT = 64 * K;    // samples per time tile
     constexpr int D = kD;
@@ -706,32 +904,40 @@ dedisp_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const int32_
         }
         if (!active) continue;
         // ---- accumulate the chunk: channel pairs alternate window buffers so the next
-        // channel's first window is read while this one is summed
+        // channel's first window is read while this one is summed.  (Round 4 tried reads
+        // one trial ahead of the adds instead, with a copy per changed window: C1 0.076
+        // vs 0.068 ms.)
         const uint32_t rows_lane = smem_addr + (uint32_t)(b * buf_bytes) + 8u * lane;
         double w0[4], w1[4];
         const u32x4 *rc = recs + (size_t)c0 * kWaves;
         u32x4 rec0 = ld_uniform(rc);
         u32x4 rec1 = nc > 1 ? ld_uniform(rc + kWaves) : rec0;
-        read_window(w0, rows_lane + (rec0[0] & 0x7fffu));
+        read_window<J>(w0, rows_lane + (rec0[0] & 0x7fffu));
         for (int ci = 0; ci < nc; ci += 2) {
             const uint32_t cb0 = rows_lane + (uint32_t)(ci * chan_bytes);
             const bool has1 = ci + 1 < nc, has2 = ci + 2 < nc, has3 = ci + 3 < nc;
             u32x4 rec2 = rec0, rec3 = rec1;
             if (has2) rec2 = ld_uniform(rc + (size_t)(ci + 2) * kWaves);  // two channels ahead
-            if (has1) prefetch_window(w1, cb0 + chan_bytes + (rec1[0] & 0x7fffu));
-            channel_trials<Tl, Ta, K>(acc, w0, rec0, cb0);
+            if (has1) prefetch_window<J>(w1, cb0 + chan_bytes + (rec1[0] & 0x7fffu));
+            channel_trials<Tl, Ta, K, J>(acc, w0, rec0, cb0);
             if (!has1) break;
-            wait_window(w1);
+            wait_window<J>(w1);
             if (has3) rec3 = ld_uniform(rc + (size_t)(ci + 3) * kWaves);
-            if (has2) prefetch_window(w0, cb0 + 2 * chan_bytes + (rec2[0] & 0x7fffu));
-            channel_trials<Tl, Ta, K>(acc, w1, rec1, cb0 + chan_bytes);
-            if (has2) wait_window(w0);
+            if (has2) prefetch_window<J>(w0, cb0 + 2 * chan_bytes + (rec2[0] & 0x7fffu));
+            channel_trials<Tl, Ta, K, J>(acc, w1, rec1, cb0 + chan_bytes);
+            if (has2) wait_window<J>(w0);
             rec0 = rec2;
             rec1 = rec3;
         }
     }
     if (!active) return;
 
+    if constexpr (STATS && !PLANE && sizeof(Ta) == 8) {
+        if (t0 + TT <= n) {  // full tile: the permlane epilogue
+            stats_full_f64<E, K>(acc, a, first, slot0, cnt, tt, lane);
+            return;
+        }
+    }
     write_outputs<Tl, Ta, K, kD, PLANE, STATS>(acc, a, first, slot0, cnt, t0, tt, lane);
 }
 
@@ -1725,6 +1931,36 @@ int plan_channels(pu_plan *p, const int64_t *shifts, size_t budget)
             i = j;
         }
     }
+    // Balance the tiles: the greedy pass leaves a short last tile (C1: 64 + 36 trials), and
+    // a launch of few workgroups per CU runs as long as its busiest CU.  Same tile count,
+    // trials dealt in whole waves (kD) as evenly as possible; kept only if every balanced
+    // tile still meets the spread limit.
+    if (first.size() > 1) {
+        const int64_t nt = (int64_t)first.size();
+        const int64_t blocks = (ndm + kD - 1) / kD;
+        std::vector<int32_t> bf, bc;
+        bool ok = true;
+        int64_t t0 = 0;
+        for (int64_t t = 0; t < nt && ok; ++t) {
+            const int64_t nb = blocks / nt + (t < blocks % nt ? 1 : 0);
+            const int64_t t1 = std::min<int64_t>(ndm, t0 + nb * kD);
+            for (int64_t c = 0; c < nchan && ok; ++c) {
+                int64_t m0 = INT64_MAX, m1 = INT64_MIN;
+                for (int64_t d = t0; d < t1; ++d) {
+                    m0 = std::min(m0, shifts[d * nchan + c]);
+                    m1 = std::max(m1, shifts[d * nchan + c]);
+                }
+                ok = t1 > t0 && m1 - m0 <= kMaxSpread;
+            }
+            bf.push_back((int32_t)t0);
+            bc.push_back((int32_t)(t1 - t0));
+            t0 = t1;
+        }
+        if (ok && t0 == ndm) {
+            first.swap(bf);
+            count.swap(bc);
+        }
+    }
     const int ndt = (int)first.size();
     std::vector<int32_t> rowlen(ndt), base((size_t)ndt * nchan);
     std::vector<int32_t> rel((size_t)ndt * nchan * kTPT);  // window shift relative to the row base
@@ -1794,6 +2030,24 @@ int plan_channels(pu_plan *p, const int64_t *shifts, size_t budget)
         return PU_EINVAL;
     }
     p->exec_adds = ndm * nchan * (int64_t)p->ntt * p->TT;
+    // LDS bytes per launch (bench.py roofline): per time tile, the staged rows (E copies of
+    // row_stride elements per channel) and, per active wave and channel, one 4 x 8-byte
+    // x 64-lane window read for the first trial and for every trial whose window differs
+    // from the previous trial's (the reload flag)
+    {
+        int64_t lds_tile = 0;
+        for (size_t t = 0; t < (size_t)ndt; ++t) {
+            lds_tile += nchan * (int64_t)E * p->row_stride * esz;
+            for (int w = 0; w < kWaves && w * kD < count[t]; ++w)
+                for (int64_t c = 0; c < nchan; ++c) {
+                    const u32x4 r = rec[(t * nchan + c) * kWaves + w];
+                    int reads = 1;
+                    for (int d = 1; d < kD; ++d) reads += (r[d >> 1] >> (16 * (d & 1))) & 0x8000u ? 1 : 0;
+                    lds_tile += reads * 4 * 64 * 8;
+                }
+        }
+        p->lds_traffic = lds_tile * p->ntt;
+    }
     int rc = PU_OK;
     if (!rc) rc = upload(&p->d_first, first);
     if (!rc) rc = upload(&p->d_count, count);
@@ -2399,7 +2653,7 @@ int pu_plan_create_ex(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t 
     p->n = n;
     p->ndm = ndm;
     const int E = 8 / kVariants[v].lds_elem;
-    p->K = E * 4;
+    p->K = E * (kVariants[v].acc_f64 && kVariants[v].lds_elem == 4 ? 2 : 4);  // dedisp_kernel's J
     p->TT = 64 * p->K;
     p->ntt = (int)((n + p->TT - 1) / p->TT);
     p->opt_u8_dma = opts->u8_dma < 0 ? 1 : opts->u8_dma;

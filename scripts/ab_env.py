@@ -33,7 +33,8 @@ for v in variants:
     kv = dict(a.split("=", 1) for a in v.split(",") if a)
     saved = {k: os.environ.get(k) for k in kv}
     os.environ.update(kv)
-    plans[v] = _hip.Plan(_hip.dtype_code(x.dtype), _hip.PU_ACC_NATIVE, cfg.nchan, cfg.nsamples, sh)
+    acc = {"native": _hip.PU_ACC_NATIVE, "f32": _hip.PU_ACC_F32, "f64": _hip.PU_ACC_F64}[os.environ.get("AB_ACC", "native")]
+    plans[v] = _hip.Plan(_hip.dtype_code(x.dtype), acc, cfg.nchan, cfg.nsamples, sh)
     for k, val in saved.items():
         if val is None:
             os.environ.pop(k, None)

@@ -2,7 +2,7 @@
 # Interleaved A/B of two builds of the library (ab/lib_<A>.so vs ab/lib_<B>.so), each round
 # in its own process:  A=head B=new CFG=C3 TRIALS=625 ROUNDS=2 bash scripts/ab_lib.sh
 set -e
-A=${A:-head}; B=${B:-new}; CFG=${CFG:-C3}; TRIALS=${TRIALS:-625}; ROUNDS=${ROUNDS:-2}
+A=${A:-head}; B=${B:-new}; CFG=${CFG:-C3}; TRIALS=${TRIALS:-625}; ROUNDS=${ROUNDS:-2}; export AB_ACC=${ACC:-native}
 for r in $(seq 1 "$ROUNDS"); do
   for v in "$A" "$B"; do
     echo "== round $r lib $v"

@@ -173,15 +173,26 @@ def test_zero_dm_small_cases(gpu):
 
 @pytest.mark.parametrize("n", [1, 2, 3, 8, 1001, 4096, 262144, 262145])
 def test_median_device_matches_numpy(gpu, n):
-    """np.median (clean.py:80) by device radix select: random, tied, signed-zero,
-    infinite and NaN series, odd and even lengths."""
+    """np.median (clean.py:80) on the device (3-launch key-histogram select): random,
+    tied, signed-zero, infinite and NaN series, odd and even lengths; a smoothed light
+    curve (the renormalisation's input: the gathered-candidates path), a constant series
+    and two tight clusters (a target bin too full to gather: the refinement path), and the
+    two middle values in distant bins."""
+    from scipy.ndimage import gaussian_filter1d
     from pulsarutils import _hip
     rng = np.random.default_rng(n)
     cases = [rng.standard_normal(n) * 1e3,
              rng.integers(-3, 4, n).astype(np.float64),             # heavy ties
              np.where(rng.random(n) < 0.5, -0.0, 0.0),                # signed zeros only
              np.concatenate([rng.standard_normal(n - 1), [np.inf]]),
-             np.abs(rng.standard_normal(n)) + 1.0]
+             np.abs(rng.standard_normal(n)) + 1.0,
+             gaussian_filter1d(rng.standard_normal(n), 101 if n > 1000 else 2) * 1e-3 + 1.0,
+             np.full(n, 3.25),
+             np.where(rng.random(n) < 0.5, 1.0, np.nextafter(1.0, 2.0))]
+    if n >= 4:
+        far = rng.standard_normal(n) * 1e-3
+        far[:2] = [-1e300, 1e300]
+        cases.append(far)
     if n > 2:
         nan = rng.standard_normal(n)
         nan[n // 3] = np.nan
@@ -232,6 +243,51 @@ def test_col_means_u8_segments(gpu, nrows, ncols):
     good = skip == 0
     with np.errstate(invalid="ignore"):
         ref = x[good].astype(np.float64).sum(axis=0) / float(good.sum())
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("nrows", [1, 3, 100, 1024, 1031])
+@pytest.mark.parametrize("ncols,ld", [(1, 1), (77, 80), (4099, 4099), (4096, 4096)])
+def test_col_means_f32_certified(gpu, nrows, ncols, ld):
+    """pu_col_means on float32 input takes the certified-quarters kernel: exact partial
+    sums summed by row quarters where a column's granularity and magnitude allow it, the
+    sequential float64 chain (one wave per column) where they do not.  Columns with a
+    tiny value beside large ones (uncertifiable: the chain's rounding is the reference's),
+    huge and tiny values, NaN / inf in a used and in a skipped row, all-zero columns, ragged
+    widths (V = 1 tails) and a padded row stride: equal to numpy's float64 mean over the
+    unskipped rows (sequential over rows, SURVEY a-R) bit for bit."""
+    import torch
+    from pulsarutils import _hip
+    rng = np.random.default_rng(nrows * 31 + ncols)
+    x = np.abs(rng.standard_normal((nrows, ld))).astype(np.float32) * 3
+    skip = (rng.random(nrows) < 0.2).astype(np.uint8)
+    if nrows > 2:
+        skip[1] = 1
+    k = min(ncols, 12)
+    cols = rng.choice(ncols, size=k, replace=False)
+    for j, c in enumerate(cols):
+        r = int(rng.integers(0, nrows))
+        kind = j % 6
+        if kind == 0:
+            x[r, c] = 1e-30                       # uncertifiable: the chain
+        elif kind == 1:
+            x[:, c] = rng.random(nrows).astype(np.float32) * np.float32(1e30)
+            x[r, c] = 1.0                          # rounds in the chain
+        elif kind == 2:
+            x[r, c] = np.nan
+        elif kind == 3 and nrows > 2:
+            x[1, c] = np.inf                       # in a skipped row: no effect
+        elif kind == 4:
+            x[:, c] = 0.0
+        else:
+            x[r, c] = -x[r, c]
+    xd, sd = torch.from_numpy(x).cuda(), torch.from_numpy(skip).cuda()
+    out = torch.empty(ncols, dtype=torch.float64, device="cuda")
+    _hip.check(_hip.lib().pu_col_means(_hip.ptr(xd), _hip.PU_F32, nrows, ncols, ld, _hip.ptr(sd), _hip.ptr(out),
+                                       _hip.stream_ptr()), "pu_col_means")
+    good = skip == 0
+    with np.errstate(invalid="ignore"):
+        ref = x[good][:, :ncols].astype(np.float64).mean(0) if good.any() else np.full(ncols, np.nan)
     np.testing.assert_array_equal(out.cpu().numpy(), ref)
 
 
