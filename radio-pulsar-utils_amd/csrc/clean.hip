@@ -364,128 +364,6 @@ colsum_u8_finish_kernel(double *__restrict__ out, int64_t ncols, int nseg, int64
     out[c] = (double)tot / ngood;
 }
 
-// Float32 column means by row quarters, certified exact (clean.py:77: numpy's mean(0) of
-// the float64 copy = a sequential float64 chain over the rows).  If every term of a column
-// is a multiple of 2^q - q the finest granularity among its nonzero values (the float32
-// ulp at the value's exponent, times 2^(trailing zeros of its significand)) - and the sum
-// of their magnitudes stays below 2^(q + 53), every partial sum of every subset is exactly
-// representable in float64: the reference's chain rounds nowhere, its result is the exact
-// sum, and any order of exact partial sums reproduces it bit for bit.  Each of the
-// workgroup's kCertWaves waves sums a quarter of the rows (V columns per lane, rows in
-// order, skipped rows left out exactly as the chain adds +0.0 for them); the quarters are
-// added in order.  A column the check cannot certify (a value too small beside the
-// column's magnitude, or NaN / inf) is recomputed by the exact chain itself, one wave per
-// column: 64 rows loaded at a time, added lane after lane (readlane) in row order.
-// (The row-sequential colmean_kernel runs one wave per SIMD at C4 and reaches 4.8 TB/s.)
-constexpr int kCertWaves = 4;
-constexpr int kCertMaxRows = 8192;  // skip flags staged in LDS
-constexpr int kCertNonfinite = -1000000;
-
-__device__ __forceinline__ int f32_granularity(float v)
-{
-    const uint32_t b = __builtin_bit_cast(uint32_t, v) & 0x7fffffffu;
-    if (b == 0) return INT32_MAX;                  // zero: no constraint
-    const uint32_t e = b >> 23;
-    if (e == 255) return kCertNonfinite;           // NaN / inf: never certified
-    const uint32_t sig = e ? (b & 0x7fffffu) | 0x800000u : b;
-    return (e ? (int)e - 150 : -149) + __builtin_ctz(sig);
-}
-
-template <int V>
-__global__ void __launch_bounds__(256)
-colmean_f32_cert_kernel(const float *__restrict__ x, int64_t nrows, int64_t col0, int64_t ncols, int64_t ld,
-                        const uint8_t *__restrict__ skip, double *__restrict__ out)
-{
-    __shared__ double s_sum[kCertWaves][64 * V];
-    __shared__ double s_abs[kCertWaves][64 * V];
-    __shared__ int s_q[kCertWaves][64 * V];
-    __shared__ int s_good[kCertWaves];
-    __shared__ uint8_t sk[kCertMaxRows];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t cb = col0 + (int64_t)blockIdx.x * 64 * V;  // the workgroup's first column
-    const int64_t c = cb + lane * V;
-    for (int64_t i = threadIdx.x; i < nrows; i += 256) sk[i] = skip ? skip[i] : 0;
-    __syncthreads();
-    const int64_t seg = (nrows + kCertWaves - 1) / kCertWaves;
-    const int64_t r0 = wave * seg;
-    const int rn = (int)max((int64_t)0, min(nrows, r0 + seg) - r0);
-    double acc[V], ab[V];
-    int q[V];
-#pragma unroll
-    for (int j = 0; j < V; ++j) {
-        acc[j] = 0.0;
-        ab[j] = 0.0;
-        q[j] = INT32_MAX;
-    }
-    int good = 0;
-    for (int i = lane; i < rn; i += 64) good += sk[r0 + i] ? 0 : 1;
-    if (c < col0 + ncols && rn > 0) {
-        auto body = [&](int i, const Vec<float, V> &v) {
-            const bool s = sk[r0 + i] != 0;
-#pragma unroll
-            for (int j = 0; j < V; ++j) {
-                const double d = static_cast<double>(v.v[j]);
-                acc[j] += s ? 0.0 : d;
-                ab[j] += s ? 0.0 : fabs(d);
-                const int g = f32_granularity(v.v[j]);
-                q[j] = s ? q[j] : min(q[j], g);
-            }
-        };
-        walk_rows<float, V, decltype(body) &, 256>(x + r0 * ld + c, ld, rn, body);
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) good += __shfl_xor(good, off);
-#pragma unroll
-    for (int j = 0; j < V; ++j) {
-        s_sum[wave][lane * V + j] = acc[j];
-        s_abs[wave][lane * V + j] = ab[j];
-        s_q[wave][lane * V + j] = q[j];
-    }
-    if (lane == 0) s_good[wave] = good;
-    __syncthreads();
-    // one column per thread (64 V <= 256 columns per workgroup)
-    int ngood = 0;
-#pragma unroll
-    for (int w = 0; w < kCertWaves; ++w) ngood += s_good[w];
-    const int t = (int)threadIdx.x;  // column index within the workgroup
-    const int64_t cc = cb + t;
-    const bool mine = t < 64 * V && cc < col0 + ncols;
-    double tot = 0.0, abt = 0.0;
-    int qm = INT32_MAX;
-    if (mine) {
-#pragma unroll
-        for (int w = 0; w < kCertWaves; ++w) {
-            tot += s_sum[w][t];
-            abt += s_abs[w][t];
-            qm = min(qm, s_q[w][t]);
-        }
-    }
-    // abt: a float64 sum of <= kCertMaxRows magnitudes, relative error < 2^-39
-    const bool cert = qm > kCertNonfinite &&
-                      (qm == INT32_MAX || abt * (1.0 + 0x1p-36) < ldexp(1.0, min(qm + 53, 1000)));
-    if (mine && cert) out[cc] = tot / static_cast<double>(ngood);
-    // the exact chain for this wave's columns that failed the check (rare)
-    uint64_t todo = __ballot(mine && !cert);
-    while (todo) {
-        const int src = __builtin_ctzll(todo);
-        todo &= todo - 1;
-        const int64_t col = cb + (t & ~63) + src;
-        double chain = 0.0;
-        for (int64_t b0 = 0; b0 < nrows; b0 += 64) {
-            const int64_t r = b0 + lane;
-            const double v = (r < nrows && !sk[r]) ? static_cast<double>(x[r * ld + col]) : 0.0;
-            const int m = (int)min((int64_t)64, nrows - b0);
-            for (int i = 0; i < m; ++i) {
-                const uint64_t bits = __builtin_bit_cast(uint64_t, v);
-                const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bits, i);
-                const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bits >> 32), i);
-                chain += __builtin_bit_cast(double, (uint64_t)lo | ((uint64_t)hi << 32));
-            }
-        }
-        if (lane == src) out[col] = chain / static_cast<double>(ngood);
-    }
-}
-
 __device__ __forceinline__ int64_t reflect_index(int64_t i, int64_t n)
 {
     // scipy 'reflect' (d c b a | a b c d | d c b a): period 2n, half-sample symmetric
@@ -840,11 +718,32 @@ __global__ void zero_cols_kernel(double *out, int64_t nrows, int64_t ld, const i
 }
 
 // ---------------------------------------------------------------- median
-// np.median of a float64 series on the device (clean.py:80), so the factor pass does not
-// wait on a host round trip: the two middle order statistics selected over
-// order-preserving 64-bit keys, then numpy's mean of them, add.reduce order
-// (0 + ((0 + a) + b)) / 2; any NaN gives NaN.  (Rounds 1-3: a six-pass radix select,
-// 8 launches.)
+// np.median of a float64 series on the device (clean.py:80), so the factor pass
+// does not wait on a host round trip.  Radix select over order-preserving 64-bit
+// keys: six digit passes (11,11,11,11,11,9 bits, high to low) narrow the key
+// prefixes of the two order statistics numpy averages (k = n/2-1 and n/2 for even
+// n, n/2 twice for odd n).  Each pass is ONE histogram kernel (LDS bins, one global
+// atomic add per non-empty bin and workgroup): its workgroups first select the
+// previous pass's bin from that pass's global histogram themselves (every workgroup
+// computes the same prefix; workgroup 0 records it), and clear the buffer the next
+// pass will fill (three rotating buffers).  A one-workgroup final kernel selects the
+// last digit.  The result is numpy's mean of the two values, add.reduce order:
+// (0 + ((0 + a) + b)) / 2; any NaN gives NaN.  8 launches (was 14).
+constexpr int kMedBitsMax = 11;
+constexpr int kMedBins = 1 << kMedBitsMax;
+constexpr int kMedPasses = 6;
+constexpr int kMedBufs = 3;
+
+struct MedState {
+    uint64_t prefix[kMedPasses + 1][2];  // key prefix of each target before pass p
+    int64_t k[kMedPasses + 1][2];        // its rank among the keys with that prefix
+    uint32_t nan;
+    uint32_t pad;
+};
+
+__host__ __device__ constexpr int med_shift(int p) { return 64 - kMedBitsMax * (p + 1) > 0 ? 64 - kMedBitsMax * (p + 1) : 0; }
+__host__ __device__ constexpr int med_bits(int p) { return 64 - kMedBitsMax * p - med_shift(p); }
+
 __device__ __forceinline__ uint64_t order_key(double d)
 {
     const uint64_t u = static_cast<uint64_t>(__double_as_longlong(d));
@@ -857,296 +756,133 @@ __device__ __forceinline__ double key_value(uint64_t k)
     return __longlong_as_double(static_cast<long long>(u));
 }
 
-// ---------------------------------------------------------------- median, 3 launches
-// Round 4: the same result (numpy's mean of the two middle order statistics, NaN if any
-// NaN) in 3 launches instead of 8, exploiting that the keys of a smoothed light curve span
-// a narrow range.  (1) per-workgroup min / max of the order-preserving keys (+ NaN count;
-// the workgroups also clear the histogram and the counters); (2) every workgroup reduces
-// those, bins its keys linearly in key space, bin = (key - kmin) >> shift with 2^14 bins
-// over [kmin, kmax] (monotone in the key: the bin order is the value order), and adds its
-// LDS histogram to the global one; the last workgroup to finish (ticket) scans it for the
-// bins of the two target ranks; (3) every workgroup appends the keys of those bins (at most
-// two adjacent non-empty bins) to a candidate list; the last one sorts the candidates
-// (LDS bitonic) and picks the ranks.  A bin that holds more than kMed2Cap keys (heavily
-// repeated or clustered values) is resolved by that workgroup alone, refining the bin
-// 14 bits at a time over the whole series (exact, only slower).
-constexpr int kMed2Bits = 14;
-constexpr int kMed2Bins = 1 << kMed2Bits;
-constexpr int kMed2Cap = 8192;
-constexpr int kMed2Grid = 256;
-
-// device-coherent load (bypasses a possibly stale L1 line): data other workgroups wrote
-// in this kernel, read after the ticket
-template <typename T>
-__device__ __forceinline__ T ld_agent(const T *p)
+__global__ void median_init_kernel(MedState *st, uint32_t *hist, int64_t n)
 {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-struct Med2Part {
-    uint64_t kmin, kmax;
-    uint64_t nan;
-};
-
-struct Med2State {
-    uint32_t ticket1, ticket2, ncand, pad;
-    uint64_t kmin;
-    int32_t shift, nan;
-    int32_t bin[2];
-    int64_t before[2];  // keys in bins below the target bin
-    int64_t k[2];       // the target ranks (numpy: n/2 - 1 and n/2, or n/2 twice)
-};
-
-__device__ __forceinline__ int med2_shift(uint64_t span)
-{
-    const int bits = span ? 64 - __clzll((long long)span) : 0;
-    return bits > kMed2Bits ? bits - kMed2Bits : 0;
-}
-
-__global__ void __launch_bounds__(256)
-med2_minmax_kernel(const double *__restrict__ x, int64_t n, Med2State *st, Med2Part *part, uint32_t *hist)
-{
-    __shared__ uint64_t smin[256], smax[256];
-    __shared__ uint32_t snan[256];
     const int t = threadIdx.x;
-    for (int i = blockIdx.x * 256 + t; i < kMed2Bins; i += gridDim.x * 256) hist[i] = 0;
-    if (blockIdx.x == 0 && t == 0) {
-        st->ticket1 = 0;
-        st->ticket2 = 0;
-        st->ncand = 0;
+    if (t == 0) {
+        st->prefix[0][0] = st->prefix[0][1] = 0;
+        st->k[0][0] = (n % 2 == 0) ? n / 2 - 1 : n / 2;
+        st->k[0][1] = n / 2;
+        st->nan = 0;
     }
-    uint64_t lo = ~uint64_t(0), hi = 0;
-    uint32_t nan = 0;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + t; i < n; i += (int64_t)gridDim.x * 256) {
-        const double d = x[i];
-        if (d != d) {
-            ++nan;
-            continue;
-        }
-        const uint64_t k = order_key(d);
-        lo = k < lo ? k : lo;
-        hi = k > hi ? k : hi;
-    }
-    smin[t] = lo;
-    smax[t] = hi;
-    snan[t] = nan;
-    __syncthreads();
-    for (int off = 128; off > 0; off >>= 1) {
-        if (t < off) {
-            smin[t] = smin[t + off] < smin[t] ? smin[t + off] : smin[t];
-            smax[t] = smax[t + off] > smax[t] ? smax[t + off] : smax[t];
-            snan[t] += snan[t + off];
-        }
-        __syncthreads();
-    }
-    if (t == 0) part[blockIdx.x] = Med2Part{smin[0], smax[0], snan[0]};
+    for (int i = t; i < kMedBufs * 2 * kMedBins; i += blockDim.x) hist[i] = 0;
 }
 
-// Reduce the per-workgroup min / max / NaN count (every thread gets the result).
-__device__ void med2_range(const Med2Part *part, int nparts, uint64_t &kmin, uint64_t &kmax, uint64_t &nan)
+// Block-wide selection (256 threads): the bin of ``hj`` holding rank k; thread t owns
+// bins [8t, 8t+8).  Returns (bin, rank inside the bin) to every thread.
+__device__ void med_select_block(const uint32_t *hj, int64_t k, uint32_t *scan, int64_t *res, int &bin,
+                                 int64_t &rem)
 {
-    __shared__ uint64_t smin[256], smax[256], snan[256];
     const int t = threadIdx.x;
-    uint64_t lo = ~uint64_t(0), hi = 0, nn = 0;
-    for (int i = t; i < nparts; i += 256) {
-        const Med2Part p = part[i];
-        lo = p.kmin < lo ? p.kmin : lo;
-        hi = p.kmax > hi ? p.kmax : hi;
-        nn += p.nan;
+    uint32_t c[8], sum = 0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        c[b] = hj[8 * t + b];
+        sum += c[b];
     }
-    smin[t] = lo;
-    smax[t] = hi;
-    snan[t] = nn;
-    __syncthreads();
-    for (int off = 128; off > 0; off >>= 1) {
-        if (t < off) {
-            smin[t] = smin[t + off] < smin[t] ? smin[t + off] : smin[t];
-            smax[t] = smax[t + off] > smax[t] ? smax[t + off] : smax[t];
-            snan[t] += snan[t + off];
-        }
-        __syncthreads();
-    }
-    kmin = smin[0];
-    kmax = smax[0];
-    nan = snan[0];
-    __syncthreads();
-}
-
-// Block scan of a histogram of kMed2Bins counts: the bin holding rank k and the count of
-// the bins below it (256 threads, 64 bins each).
-__device__ void med2_find(const uint32_t *h, int64_t k, int &bin, int64_t &before)
-{
-    __shared__ int64_t scan[256];
-    __shared__ int64_t res[2];
-    const int t = threadIdx.x;
-    constexpr int PER = kMed2Bins / 256;
-    int64_t sum = 0;
-    for (int b = 0; b < PER; ++b) sum += ld_agent(h + t * PER + b);
     scan[t] = sum;
     __syncthreads();
     for (int off = 1; off < 256; off <<= 1) {
-        const int64_t v = t >= off ? scan[t - off] : 0;
+        const uint32_t v = t >= off ? scan[t - off] : 0;
         __syncthreads();
         scan[t] += v;
         __syncthreads();
     }
-    const int64_t start = scan[t] - sum;
-    if (k >= start && k < start + sum) {
-        int64_t c = start;
+    const int64_t before = (int64_t)scan[t] - sum;
+    if (k >= before && k < before + (int64_t)sum) {
+        int64_t r = k - before;
         int b = 0;
-        while (c + (int64_t)ld_agent(h + t * PER + b) <= k) c += ld_agent(h + t * PER + b++);
-        res[0] = t * PER + b;
-        res[1] = c;
+        while (r >= (int64_t)c[b]) r -= c[b++];
+        res[0] = 8 * t + b;
+        res[1] = r;
     }
     __syncthreads();
     bin = (int)res[0];
-    before = res[1];
+    rem = res[1];
     __syncthreads();
 }
 
-__global__ void __launch_bounds__(256)
-med2_hist_kernel(const double *__restrict__ x, int64_t n, Med2State *st, const Med2Part *part, uint32_t *hist)
+// Prefix and rank of both targets before pass ``pass`` (pass >= 1), from the previous
+// pass's histogram.
+__device__ void med_prefix(const MedState *st, const uint32_t *hist, int pass, uint32_t *scan, int64_t *res,
+                           uint64_t (&pfx)[2], int64_t (&kk)[2])
 {
-    __shared__ uint32_t h[kMed2Bins];
-    __shared__ int last;
-    uint64_t kmin, kmax, nan;
-    med2_range(part, gridDim.x, kmin, kmax, nan);
-    const int t = threadIdx.x;
-    const int shift = med2_shift(kmax - kmin);
-    if (nan == 0) {
-        for (int i = t; i < kMed2Bins; i += 256) h[i] = 0;
-        __syncthreads();
-        for (int64_t i = (int64_t)blockIdx.x * 256 + t; i < n; i += (int64_t)gridDim.x * 256)
-            atomicAdd(&h[(uint32_t)((order_key(x[i]) - kmin) >> shift)], 1u);
-        __syncthreads();
-        for (int i = t; i < kMed2Bins; i += 256)
-            if (h[i]) atomicAdd(&hist[i], h[i]);
-    }
-    __threadfence();
-    __syncthreads();
-    if (t == 0) last = atomicAdd(&st->ticket1, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    const int64_t kk[2] = {n % 2 == 0 ? n / 2 - 1 : n / 2, n / 2};
-    int b[2] = {0, 0};
-    int64_t before[2] = {0, 0};
-    if (nan == 0)
-        for (int j = 0; j < 2; ++j) med2_find(hist, kk[j], b[j], before[j]);
-    if (t == 0) {
-        st->kmin = kmin;
-        st->shift = shift;
-        st->nan = nan ? 1 : 0;
-        for (int j = 0; j < 2; ++j) {
-            st->bin[j] = b[j];
-            st->before[j] = before[j];
-            st->k[j] = kk[j];
-        }
-    }
-}
-
-// One workgroup: the key of rank k among all non-NaN keys, by histogram refinement over
-// the whole series (the slow exact path for a target bin too full to gather).
-__device__ uint64_t med2_select_slow(const double *x, int64_t n, uint64_t lo, int shift, int64_t k, uint32_t *h)
-{
-    __shared__ uint64_t res_lo;
-    const int t = threadIdx.x;
-    for (;;) {
-        const int sh2 = shift > kMed2Bits ? shift - kMed2Bits : 0;  // the refined bins
-        const uint64_t width = uint64_t(1) << shift;                // the current bin's key width
-        for (int i = t; i < kMed2Bins; i += 256) h[i] = 0;
-        __syncthreads();
-        int64_t below = 0;  // keys under lo (rank offset of the bin)
-        for (int64_t i = t; i < n; i += 256) {
-            const double d = x[i];
-            if (d != d) continue;
-            const uint64_t key = order_key(d);
-            if (key < lo) ++below;
-            else if (key - lo < width) atomicAdd(&h[(uint32_t)((key - lo) >> sh2)], 1u);
-        }
-        __shared__ int64_t red[256];
-        red[t] = below;
-        __syncthreads();
-        for (int off = 128; off > 0; off >>= 1) {
-            if (t < off) red[t] += red[t + off];
-            __syncthreads();
-        }
-        const int64_t kr = k - red[0];
-        __syncthreads();
+    const uint32_t *hp = hist + (size_t)((pass - 1) % kMedBufs) * 2 * kMedBins;
+    for (int j = 0; j < 2; ++j) {
         int bin;
-        int64_t before;
-        med2_find(h, kr, bin, before);
-        if (t == 0) res_lo = lo + ((uint64_t)bin << sh2);
-        __syncthreads();
-        lo = res_lo;
-        if (sh2 == 0) return lo;
-        shift = sh2;
-        __syncthreads();
+        int64_t rem;
+        med_select_block(hp + j * kMedBins, st->k[pass - 1][j], scan, res, bin, rem);
+        pfx[j] = st->prefix[pass - 1][j] | ((uint64_t)bin << med_shift(pass - 1));
+        kk[j] = rem;
     }
 }
 
 __global__ void __launch_bounds__(256)
-med2_gather_kernel(const double *__restrict__ x, int64_t n, Med2State *st, uint64_t *cand, uint32_t *hist,
-                   double *out)
+median_hist_kernel(const double *__restrict__ x, int64_t n, MedState *st, uint32_t *hist, int pass)
 {
-    __shared__ int last;
-    __shared__ uint64_t v[kMed2Cap];
-    const int t = threadIdx.x;
-    const Med2State s = *st;
-    if (s.nan) {
-        if (blockIdx.x == 0 && t == 0) out[0] = __longlong_as_double(0x7ff8000000000000ll);
+    __shared__ uint32_t h[2][kMedBins];
+    __shared__ uint32_t scan[256];
+    __shared__ int64_t res[2];
+    uint64_t pfx[2] = {0, 0};
+    int64_t kk[2] = {st->k[0][0], st->k[0][1]};
+    if (pass > 0) {
+        med_prefix(st, hist, pass, scan, res, pfx, kk);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            st->prefix[pass][0] = pfx[0];
+            st->prefix[pass][1] = pfx[1];
+            st->k[pass][0] = kk[0];
+            st->k[pass][1] = kk[1];
+        }
+    }
+    // clear the buffer the NEXT pass accumulates into (nobody reads it during this pass)
+    uint32_t *nxt = hist + (size_t)((pass + 1) % kMedBufs) * 2 * kMedBins;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < 2 * kMedBins; i += gridDim.x * 256) nxt[i] = 0;
+    for (int i = threadIdx.x; i < 2 * kMedBins; i += 256) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const int shift = med_shift(pass), bits = med_bits(pass);
+    const uint64_t dmask = (uint64_t(1) << bits) - 1;
+    const int hs = shift + bits;  // bits above the digit must match the prefix
+    uint32_t nans = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const double d = x[i];
+        if (d != d) {
+            ++nans;
+            continue;
+        }
+        const uint64_t k = order_key(d);
+        const uint32_t dig = (uint32_t)((k >> shift) & dmask);
+        if (hs >= 64 || (k >> hs) == (pfx[0] >> hs)) atomicAdd(&h[0][dig], 1u);
+        if (hs >= 64 || (k >> hs) == (pfx[1] >> hs)) atomicAdd(&h[1][dig], 1u);
+    }
+    if (pass == 0 && nans) atomicAdd(&st->nan, nans);
+    __syncthreads();
+    uint32_t *cur = hist + (size_t)(pass % kMedBufs) * 2 * kMedBins;
+    for (int i = threadIdx.x; i < 2 * kMedBins; i += 256) {
+        const uint32_t c = (&h[0][0])[i];
+        if (c) atomicAdd(&cur[i], c);
+    }
+}
+
+// One workgroup: the last digit, then numpy's mean of the two order statistics.
+__global__ void __launch_bounds__(256) median_final_kernel(MedState *st, const uint32_t *hist, int64_t n,
+                                                           double *out)
+{
+    __shared__ uint32_t scan[256];
+    __shared__ int64_t res[2];
+    uint64_t pfx[2];
+    int64_t kk[2];
+    med_prefix(st, hist, kMedPasses, scan, res, pfx, kk);
+    if (threadIdx.x != 0) return;
+    if (st->nan) {
+        out[0] = __longlong_as_double(0x7ff8000000000000ll);
         return;
     }
-    const uint32_t b0 = (uint32_t)s.bin[0], b1 = (uint32_t)s.bin[1];
-    const int64_t nc = (int64_t)hist[b0] + (b1 != b0 ? (int64_t)hist[b1] : 0);
-    if (nc <= kMed2Cap) {
-        for (int64_t i = (int64_t)blockIdx.x * 256 + t; i < n; i += (int64_t)gridDim.x * 256) {
-            const uint64_t key = order_key(x[i]);
-            const uint32_t b = (uint32_t)((key - s.kmin) >> s.shift);
-            if (b == b0 || b == b1) cand[atomicAdd(&st->ncand, 1u)] = key;
-        }
-    }
-    __threadfence();
-    __syncthreads();
-    if (t == 0) last = atomicAdd(&st->ticket2, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    uint64_t key[2];
-    if (nc <= kMed2Cap) {
-        int m = 1;
-        while (m < nc) m <<= 1;
-        for (int i = t; i < m; i += 256) v[i] = i < nc ? ld_agent(cand + i) : ~uint64_t(0);
-        __syncthreads();
-        for (int kb = 2; kb <= m; kb <<= 1)
-            for (int j = kb >> 1; j > 0; j >>= 1) {
-                for (int i = t; i < m; i += 256) {
-                    const int l = i ^ j;
-                    if (l > i) {
-                        const uint64_t a = v[i], b = v[l];
-                        if (((i & kb) == 0) ? (b < a) : (a < b)) {
-                            v[i] = b;
-                            v[l] = a;
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-        key[0] = v[s.k[0] - s.before[0]];
-        key[1] = v[s.k[1] - s.before[0]];  // b1 is b0 or the next non-empty bin
+    const double a = key_value(pfx[0]);
+    if (n % 2 == 0) {
+        const double b = key_value(pfx[1]);
+        out[0] = (0.0 + ((0.0 + a) + b)) / 2.0;
     } else {
-        uint32_t *h = reinterpret_cast<uint32_t *>(v);  // kMed2Bins counters in the candidate area
-        for (int j = 0; j < 2; ++j)
-            key[j] = med2_select_slow(x, n, s.kmin + ((uint64_t)s.bin[j] << s.shift), s.shift, s.k[j], h);
-    }
-    if (t == 0) {
-        const double a = key_value(key[0]);
-        if (n % 2 == 0) {
-            const double b = key_value(key[1]);
-            out[0] = (0.0 + ((0.0 + a) + b)) / 2.0;
-        } else {
-            out[0] = (0.0 + (0.0 + a)) / 1.0;
-        }
+        out[0] = (0.0 + (0.0 + a)) / 1.0;
     }
 }
 
@@ -1375,19 +1111,6 @@ int col_means_t(const void *x, int64_t nrows, int64_t n, int64_t ld, const uint8
             return PU_OK;
         }
     }
-    if constexpr (std::is_same<Tin, float>::value) {
-        // certified quarters (exact whenever the column's values allow it, else the chain);
-        // PU_COLCERT=0 (diagnostic build): the row-sequential kernel
-        static const bool cert = pu::knob("PU_COLCERT", 1) != 0;
-        if (cert && nrows <= kCertMaxRows) {
-            const int v = pick_vec<float>(x, ld, 4);
-            return column_launches<float>(v, n, [&](auto vc, int64_t col0, int64_t ncols) {
-                constexpr int V = decltype(vc)::value;
-                hipLaunchKernelGGL((colmean_f32_cert_kernel<V>), dim3(blocks_for(ncols, 64 * V)), dim3(256), 0, s,
-                                   reinterpret_cast<const float *>(x), nrows, col0, ncols, ld, skip, out);
-            });
-        }
-    }
     const int v = pick_vec<Tin>(x, ld, vec_max(sizeof(Tin), 4));
     // bytes of rows in flight per lane and register buffer (PU_CLEAN_BATCH: 128, 256 or 512)
     int bb = 256;  // C4 sweep (profiles/r02_clean/): f32 V=4 190 us vs 212 us at 128 B
@@ -1577,11 +1300,7 @@ int pu_cut_outliers(const double *lc, int64_t n, double *out, int64_t nrows, int
     return pu::launch_check("outlier kernels");
 }
 
-size_t pu_median_workspace_bytes(void)
-{
-    return sizeof(Med2State) + kMed2Grid * sizeof(Med2Part) + kMed2Bins * sizeof(uint32_t) +
-           kMed2Cap * sizeof(uint64_t);
-}
+size_t pu_median_workspace_bytes(void) { return sizeof(MedState) + kMedBufs * 2 * kMedBins * sizeof(uint32_t); }
 
 int pu_median(const double *x, int64_t n, double *out, void *ws, size_t ws_bytes, void *stream)
 {
@@ -1589,14 +1308,17 @@ int pu_median(const double *x, int64_t n, double *out, void *ws, size_t ws_bytes
     PU_REQUIRE(ws && ws_bytes >= pu_median_workspace_bytes(), "pu_median: workspace too small");
     PU_REQUIRE(reinterpret_cast<uintptr_t>(ws) % 8 == 0, "pu_median: workspace not 8-byte aligned");
     hipStream_t s = pu::as_stream(stream);
-    Med2State *st = reinterpret_cast<Med2State *>(ws);
-    Med2Part *part = reinterpret_cast<Med2Part *>(st + 1);
-    uint32_t *hist = reinterpret_cast<uint32_t *>(part + kMed2Grid);
-    uint64_t *cand = reinterpret_cast<uint64_t *>(hist + kMed2Bins);
-    const unsigned grid = (unsigned)std::min<int64_t>(kMed2Grid, std::max<int64_t>(1, (n + 1023) / 1024));
-    hipLaunchKernelGGL(med2_minmax_kernel, dim3(grid), dim3(256), 0, s, x, n, st, part, hist);
-    hipLaunchKernelGGL(med2_hist_kernel, dim3(grid), dim3(256), 0, s, x, n, st, part, hist);
-    hipLaunchKernelGGL(med2_gather_kernel, dim3(grid), dim3(256), 0, s, x, n, st, cand, hist, out);
+    MedState *st = reinterpret_cast<MedState *>(ws);
+    uint32_t *hist = reinterpret_cast<uint32_t *>(st + 1);
+    hipLaunchKernelGGL(median_init_kernel, dim3(1), dim3(256), 0, s, st, hist, n);
+    // a few elements per thread: fewer workgroups to flush LDS bins to the global histogram
+    // (PU_MEDIAN_GRID: most workgroups per pass, tuning)
+    int64_t gmax = 256;
+    gmax = std::max(1, pu::knob("PU_MEDIAN_GRID", (int)gmax));
+    const unsigned grid = std::min<int64_t>(gmax, std::max<int64_t>(1, (n + 1023) / 1024));
+    for (int p = 0; p < kMedPasses; ++p)
+        hipLaunchKernelGGL(median_hist_kernel, dim3(grid), dim3(256), 0, s, x, n, st, hist, p);
+    hipLaunchKernelGGL(median_final_kernel, dim3(1), dim3(256), 0, s, st, hist, n, out);
     return pu::launch_check("median_kernels");
 }
 

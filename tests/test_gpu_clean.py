@@ -173,11 +173,10 @@ def test_zero_dm_small_cases(gpu):
 
 @pytest.mark.parametrize("n", [1, 2, 3, 8, 1001, 4096, 262144, 262145])
 def test_median_device_matches_numpy(gpu, n):
-    """np.median (clean.py:80) on the device (3-launch key-histogram select): random,
-    tied, signed-zero, infinite and NaN series, odd and even lengths; a smoothed light
-    curve (the renormalisation's input: the gathered-candidates path), a constant series
-    and two tight clusters (a target bin too full to gather: the refinement path), and the
-    two middle values in distant bins."""
+    """np.median (clean.py:80) by device radix select: random, tied, signed-zero,
+    infinite and NaN series, odd and even lengths, a smoothed light curve (the
+    renormalisation's input), a constant series, two tight clusters and the two middle
+    values far apart in key space."""
     from scipy.ndimage import gaussian_filter1d
     from pulsarutils import _hip
     rng = np.random.default_rng(n)
@@ -249,13 +248,12 @@ def test_col_means_u8_segments(gpu, nrows, ncols):
 @pytest.mark.parametrize("nrows", [1, 3, 100, 1024, 1031])
 @pytest.mark.parametrize("ncols,ld", [(1, 1), (77, 80), (4099, 4099), (4096, 4096)])
 def test_col_means_f32_certified(gpu, nrows, ncols, ld):
-    """pu_col_means on float32 input takes the certified-quarters kernel: exact partial
-    sums summed by row quarters where a column's granularity and magnitude allow it, the
-    sequential float64 chain (one wave per column) where they do not.  Columns with a
-    tiny value beside large ones (uncertifiable: the chain's rounding is the reference's),
-    huge and tiny values, NaN / inf in a used and in a skipped row, all-zero columns, ragged
-    widths (V = 1 tails) and a padded row stride: equal to numpy's float64 mean over the
-    unskipped rows (sequential over rows, SURVEY a-R) bit for bit."""
+    """pu_col_means on float32 input (the zero-DM light curve, clean.py:77: numpy's
+    float64 mean(0), a sequential chain over the rows): columns with a tiny value beside
+    large ones, huge and tiny values (the chain's roundings), NaN / inf in a used and in a
+    skipped row, all-zero columns, ragged widths (V = 1 tails) and a padded row stride:
+    equal to numpy bit for bit.  (Round 4 also ran a row-quarters kernel certified exact
+    per column against it: 268 vs 236 us at C4, not kept; profiles/r04/experiments/.)"""
     import torch
     from pulsarutils import _hip
     rng = np.random.default_rng(nrows * 31 + ncols)
