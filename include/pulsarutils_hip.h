@@ -87,8 +87,7 @@ typedef struct pu_plan_opts {
     int32_t lds_budget_kb;  /* 0: default (160 KiB subband, 64 KiB channel mode) */
     int32_t u8_dma;         /* -1 auto (8-bit rows by LDS-DMA when n % 4 == 0), 0 global-memory build */
     int32_t dt_major;       /* -1 auto item order, 0 time-tile major, 1 DM-tile major */
-    int32_t build;          /* slot build of 8-bit plans: 1 select build where eligible, 0 / -1 direct */
-    int32_t reserved[2];    /* zero */
+    int32_t reserved[3];    /* zero */
 } pu_plan_opts;
 int pu_plan_create_ex(pu_plan **plan, int dtype, int acc, int64_t nchan, int64_t nsamples,
                       const int64_t *shifts, int64_t ndm, const pu_plan_opts *opts);
@@ -257,15 +256,20 @@ int pu_renorm_apply_zero_dm(const void *x, int dtype, int64_t nchan, int64_t n, 
  * means lc[n] of the renormalised plane (pu_renorm_apply's col_means), mask[t] =
  * uniform_filter1d(lc, 16)[t] > 5 sd  or  < -3 sd, sd = np.std(uniform_filter1d(lc,
  * 16)[::16]), and out[:, t] = 0 where mask[t].  scipy's running-sum order is not
- * reproducible in parallel: every decision is made on directly summed windows and
- * CERTIFIED against a rigorous rounding bound of both orders; a decision closer to
- * its threshold than the bound (or a NaN) sets the flag word ws[0:4] (uint32) and the
- * caller must redo the step on the host (scipy) from a fresh apply pass.  ws[4:8]
- * (uint32) = number of bad bins.  n >= 64; ws: pu_cut_outliers_workspace_bytes(n),
- * 8-byte aligned. */
+ * reproducible in parallel: every decision is first made on directly summed windows and
+ * CERTIFIED against a rigorous rounding bound of both orders; when a decision is closer
+ * to its threshold than the bound (or a value is NaN) the flag word ws[0:4] (uint32) is
+ * set and a one-workgroup kernel on the same stream recomputes the mask with scipy's and
+ * numpy's own arithmetic (running sum, add.reduce order).  Either way the mask and the
+ * zeroed columns are the reference's, with no host round trip (round 4: the caller used
+ * to redo the step with scipy).  ws[4:8] (uint32) = number of bad bins.  n >= 64; ws:
+ * pu_cut_outliers_workspace_bytes(n), 8-byte aligned.
+ * pu_cut_outliers_exact: the exact path only (testing, or callers that want it). */
 size_t pu_cut_outliers_workspace_bytes(int64_t n);
 int pu_cut_outliers(const double *lc, int64_t n, double *out, int64_t nrows, int64_t ld_out,
                     uint8_t *mask, void *workspace, size_t workspace_bytes, void *stream);
+int pu_cut_outliers_exact(const double *lc, int64_t n, double *out, int64_t nrows, int64_t ld_out,
+                          uint8_t *mask, void *workspace, size_t workspace_bytes, void *stream);
 
 /* out[:, cols[k]] = 0 for k < ncols (clean.py:105). cols: device int64. */
 int pu_zero_columns(double *out, int64_t nrows, int64_t ld_out, const int64_t *cols,

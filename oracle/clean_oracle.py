@@ -124,3 +124,44 @@ def apply_dm_shifts(data, shifts):
     for i in range(data.shape[0]):
         out[i] = np.roll(data[i], -int(np.rint(shifts[i])))
     return out
+
+
+def uniform_filter1d_running(lc, size=16):
+    """scipy.ndimage.uniform_filter1d(lc, size) (mode 'reflect', origin 0) restated as
+    scipy's running sum (ni_filters.c NI_UniformFilter1D): the first window summed from
+    0.0 and divided by size, then tmp += (x[i + size - 1 - size//2] - x[i - 1 - size//2])
+    / size over the reflected line.  The order csrc/clean.hip outlier_exact_kernel
+    follows."""
+    lc = np.asarray(lc, dtype=np.float64)
+    n = lc.size
+    s1 = size // 2
+
+    def ext(k):
+        i = k - s1
+        if i < 0:
+            i = -i - 1
+        if i >= n:
+            i = 2 * n - 1 - i
+        return lc[i]
+
+    out = np.empty(n)
+    tmp = 0.0
+    for j in range(size):
+        tmp += ext(j)
+    tmp /= size
+    out[0] = tmp
+    for i in range(1, n):
+        tmp += (ext(i + size - 1) - ext(i - 1)) / size
+        out[i] = tmp
+    return out
+
+
+def std_numpy_order(v):
+    """np.std(v) restated: numpy add.reduce order (oracle/numpy_order.py) for the mean
+    and for the squared deviations, true divides, sqrt."""
+    from .numpy_order import reduce_sum
+    v = np.ascontiguousarray(v, dtype=np.float64)
+    m = v.size
+    mean = reduce_sum(v) / m
+    d = v - mean
+    return np.sqrt(reduce_sum(d * d) / m)

@@ -672,11 +672,119 @@ __global__ void __launch_bounds__(1024) outlier_std_kernel(const double *__restr
     }
 }
 
-// Per 64 columns: wave 0 decides (certified) and records the mask; then the block
-// zeroes the bad columns of the plane (rows strided over the 4 waves).
+// Certified decisions, one lane per time bin: the mask and the flag (an ambiguous
+// comparison raises it; outlier_exact_kernel then redoes the mask).
 __global__ void __launch_bounds__(256)
-outlier_mask_zero_kernel(const double *__restrict__ u, int64_t n, OutlierState *st, uint8_t *__restrict__ mask,
-                         double *__restrict__ out, int64_t nrows, int64_t ld)
+outlier_mask_kernel(const double *__restrict__ u, int64_t n, OutlierState *st, uint8_t *__restrict__ mask)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const double v = u[i];
+    const double du = v - st->up, dd = v - st->down;
+    const bool amb = !(fabs(du) > st->margin_up) || !(fabs(dd) > st->margin_down);
+    if (amb) atomicOr(&st->flag, 1u);
+    const uint8_t b = (du > 0.0 || dd < 0.0) ? 1 : 0;
+    mask[i] = b;
+    if (b) atomicAdd(&st->nbad, 1u);
+}
+
+// numpy add.reduce of a contiguous double vector (0 + pairwise sums of 8192-element
+// blocks) by one lane; each block is staged in LDS by the whole workgroup first.
+__device__ double reduce_sum_staged(const double *__restrict__ a, int64_t m, double *stage)
+{
+    double acc = 0.0;
+    for (int64_t b = 0; b < m; b += kBlock) {
+        const int len = (int)(m - b < kBlock ? m - b : kBlock);
+        __syncthreads();
+        for (int k = threadIdx.x; k < len; k += blockDim.x) stage[k] = a[b + k];
+        __syncthreads();
+        if (threadIdx.x == 0) acc += pairwise_lane<double, double, 0, 10>(stage, 0, len, 0.0, nullptr);
+    }
+    return acc;  // valid in lane 0
+}
+
+// The reference's own arithmetic for the rare case (the flag is set: a certified decision
+// was ambiguous, or the light curve holds NaN / inf), on the device so that the common
+// path needs no host round trip (round 4; the host used to rerun scipy).  One
+// workgroup:
+//  * scipy.ndimage.uniform_filter1d(lc, 16) (mode 'reflect', origin 0): the running sum
+//    tmp = (sum of the first window) / 16, then tmp += (x[i + 7] - x[i - 9]) / 16 - the
+//    differences of a chunk by all lanes into LDS (each is scipy's single rounding),
+//    the chain by lane 0 (its order is the whole point);
+//  * np.std(lc_rebin[::16]): numpy's add.reduce order for the mean and for the squared
+//    deviations (a compact copy in tmp);
+//  * bad = lc_rebin > 5 sd | lc_rebin < -3 sd (NaN compares false, as in numpy).
+// Restatement checked bit for bit against scipy / numpy on CPU
+// (tests/test_oracle.py::test_cut_outliers_exact_restatement).
+__global__ void __launch_bounds__(256)
+outlier_exact_kernel(const double *__restrict__ lc, int64_t n, OutlierState *st, double *__restrict__ v,
+                     double *__restrict__ tmp, uint8_t *__restrict__ mask, int force)
+{
+    if (!force && st->flag == 0) return;
+    __shared__ double stage[kBlock];
+    __shared__ double thr[2];
+    constexpr int kSize = 16, kOrig = kSize / 2;  // window [i - 8, i + 7]
+    const int t = threadIdx.x;
+    auto ext = [&](int64_t k) { return lc[reflect_small(k - kOrig, n)]; };  // scipy's extended line
+    double s = 0.0;
+    if (t == 0) {
+        for (int j = 0; j < kSize; ++j) s += ext(j);
+        s /= (double)kSize;
+        v[0] = s;
+    }
+    for (int64_t c0 = 1; c0 < n; c0 += kBlock) {
+        const int len = (int)(n - c0 < kBlock ? n - c0 : kBlock);
+        __syncthreads();
+        for (int k = t; k < len; k += 256) stage[k] = (ext(c0 + k + kSize - 1) - ext(c0 + k - 1)) / (double)kSize;
+        __syncthreads();
+        if (t == 0)
+            for (int k = 0; k < len; ++k) {
+                s += stage[k];
+                v[c0 + k] = s;
+            }
+    }
+    __syncthreads();
+    __threadfence_block();
+    const int64_t m = (n + 15) / 16;
+    for (int64_t k = t; k < m; k += 256) tmp[k] = v[16 * k];
+    __threadfence_block();
+    const double mean = reduce_sum_staged(tmp, m, stage) / (double)m;  // lane 0
+    __syncthreads();
+    if (t == 0) thr[0] = mean;
+    __syncthreads();
+    for (int64_t k = t; k < m; k += 256) {
+        const double d = tmp[k] - thr[0];
+        tmp[k] = d * d;
+    }
+    __threadfence_block();
+    const double ss = reduce_sum_staged(tmp, m, stage);
+    __syncthreads();
+    if (t == 0) {
+        const double sd = sqrt(ss / (double)m);
+        thr[0] = 5.0 * sd;
+        thr[1] = -3.0 * sd;
+        st->sd = sd;
+        st->up = thr[0];
+        st->down = thr[1];
+        st->nbad = 0;
+        st->flag = 1;
+    }
+    __syncthreads();
+    __threadfence_block();
+    unsigned cnt = 0;
+    for (int64_t i = t; i < n; i += 256) {
+        const double x = v[i];
+        const uint8_t b = (x > thr[0] || x < thr[1]) ? 1 : 0;
+        mask[i] = b;
+        cnt += b;
+    }
+    if (cnt) atomicAdd(&st->nbad, cnt);
+}
+
+// Per 64 columns: zero the plane's bad columns (the final mask), rows strided over the
+// block's 4 waves.
+__global__ void __launch_bounds__(256)
+outlier_zero_kernel(const uint8_t *__restrict__ mask, int64_t n, double *__restrict__ out, int64_t nrows, int64_t ld)
 {
     __shared__ uint8_t bad[64];
     __shared__ int any;
@@ -685,26 +793,14 @@ outlier_mask_zero_kernel(const double *__restrict__ u, int64_t n, OutlierState *
     if (t == 0) any = 0;
     __syncthreads();
     if (t < 64) {
-        const int64_t i = c0 + t;
-        uint8_t b = 0;
-        if (i < n) {
-            const double v = u[i];
-            const double du = v - st->up, dd = v - st->down;
-            const bool amb = !(fabs(du) > st->margin_up) || !(fabs(dd) > st->margin_down);
-            if (amb) atomicOr(&st->flag, 1u);
-            b = (du > 0.0 || dd < 0.0) ? 1 : 0;
-            mask[i] = b;
-            if (b) {
-                atomicAdd(&st->nbad, 1u);
-                any = 1;
-            }
-        }
+        const uint8_t b = c0 + t < n ? mask[c0 + t] : 0;
         bad[t] = b;
+        if (b) any = 1;
     }
     __syncthreads();
     if (!any) return;
     const int col = t & 63;
-    if (!bad[col] || c0 + col >= n) return;
+    if (!bad[col]) return;
     for (int64_t r = t >> 6; r < nrows; r += 4) out[r * ld + c0 + col] = 0.0;
 }
 
@@ -1282,8 +1378,9 @@ size_t pu_cut_outliers_workspace_bytes(int64_t n)
     return 256 + (m + (m + 15) / 16) * sizeof(double);  // state | window means | every 16th
 }
 
-int pu_cut_outliers(const double *lc, int64_t n, double *out, int64_t nrows, int64_t ld_out, uint8_t *mask,
-                    void *ws, size_t ws_bytes, void *stream)
+namespace {
+int cut_outliers(const double *lc, int64_t n, double *out, int64_t nrows, int64_t ld_out, uint8_t *mask, void *ws,
+                 size_t ws_bytes, void *stream, bool exact_only)
 {
     PU_REQUIRE(lc && out && mask && n >= 64 && nrows > 0 && ld_out >= n, "pu_cut_outliers: bad arguments");
     PU_REQUIRE(ws && ws_bytes >= pu_cut_outliers_workspace_bytes(n) && reinterpret_cast<uintptr_t>(ws) % 8 == 0,
@@ -1293,11 +1390,28 @@ int pu_cut_outliers(const double *lc, int64_t n, double *out, int64_t nrows, int
     double *u = reinterpret_cast<double *>(reinterpret_cast<char *>(ws) + 256);
     double *u16 = u + n;
     PU_TRY_HIP(hipMemsetAsync(st, 0, sizeof(OutlierState), s));
-    hipLaunchKernelGGL(outlier_window_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, lc, n, u, u16, st);
-    hipLaunchKernelGGL(outlier_std_kernel, dim3(1), dim3(1024), 0, s, u16, n, st);
-    hipLaunchKernelGGL(outlier_mask_zero_kernel, dim3(blocks_for(n, 64)), dim3(256), 0, s, u, n, st, mask, out,
-                       nrows, ld_out);
+    if (!exact_only) {
+        hipLaunchKernelGGL(outlier_window_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, lc, n, u, u16, st);
+        hipLaunchKernelGGL(outlier_std_kernel, dim3(1), dim3(1024), 0, s, u16, n, st);
+        hipLaunchKernelGGL(outlier_mask_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, u, n, st, mask);
+    }
+    // returns at once unless the flag is set (or exact_only)
+    hipLaunchKernelGGL(outlier_exact_kernel, dim3(1), dim3(256), 0, s, lc, n, st, u, u16, mask, exact_only ? 1 : 0);
+    hipLaunchKernelGGL(outlier_zero_kernel, dim3(blocks_for(n, 64)), dim3(256), 0, s, mask, n, out, nrows, ld_out);
     return pu::launch_check("outlier kernels");
+}
+}  // namespace
+
+int pu_cut_outliers(const double *lc, int64_t n, double *out, int64_t nrows, int64_t ld_out, uint8_t *mask,
+                    void *ws, size_t ws_bytes, void *stream)
+{
+    return cut_outliers(lc, n, out, nrows, ld_out, mask, ws, ws_bytes, stream, false);
+}
+
+int pu_cut_outliers_exact(const double *lc, int64_t n, double *out, int64_t nrows, int64_t ld_out, uint8_t *mask,
+                          void *ws, size_t ws_bytes, void *stream)
+{
+    return cut_outliers(lc, n, out, nrows, ld_out, mask, ws, ws_bytes, stream, true);
 }
 
 size_t pu_median_workspace_bytes(void) { return sizeof(MedState) + kMedBufs * 2 * kMedBins * sizeof(uint32_t); }

@@ -990,12 +990,6 @@ auto with_shape(int shape, F &&f)
 // to a whole s_load.
 __host__ __device__ constexpr int slot_stride(int G) { return G <= 4 ? 8 : 16; }
 
-// Select build of 8-bit slots (plan_sub, sub_item build_sel): per channel and group the
-// slots' relative offsets lie in a window of kSelCand consecutive samples
-constexpr int kSelCand = 3;
-constexpr int kSelHdr = 4;     // group record header ints (slot begin, slots, gs, pair begin)
-constexpr int kSelPos = 128;   // positions per select-build unit (2 chunks of 64)
-
 struct SubArgs {
     DedispArgs o;           // data, ld, nchan, n, ndt, ntt, small_n; plane / partials
     int32_t ngroups;
@@ -1007,11 +1001,6 @@ struct SubArgs {
     int32_t nitems;         // work items (DM tiles x time tiles of this launch)
     int32_t base_bits;      // DMA row words: base = word & (2^base_bits - 1), cover = (word >> base_bits) x 256 B
     int32_t dt_major;       // item order: 0 = time tile major (DM tiles of a time tile share L2), 1 = DM tile major
-    int32_t sel;            // select build (8-bit DMA plans): stage records index units, not slots
-    int32_t gstride;        // select build: ints per group record
-    const i32x4 *units;     // select build: {group record, first position}
-    const int32_t *grecs;   // select build: group records
-    const uint32_t *sels;   // select build: v_perm selectors, G per pair of slots
     void *stamps;           // diagnostic build (PU_STAMPS): 8 x u64 phase-cycle totals
 };
 
@@ -1119,18 +1108,11 @@ __device__ __forceinline__ void dma_row_f32(unsigned char *dst, const float *row
         for (; off + 1024 <= cover_bytes; off += 1024)
             __builtin_amdgcn_global_load_lds((const void *)(src + off + 16 * lane),
                                              (__attribute__((address_space(3))) void *)(dst + off), 16, 0, 0);
-#ifdef PU_DMA_TAIL16
-        // experiment: the tail as one partial 16-B/lane piece
-        if (off < cover_bytes && lane < (cover_bytes - off) / 16)
-            __builtin_amdgcn_global_load_lds((const void *)(src + off + 16 * lane),
-                                             (__attribute__((address_space(3))) void *)(dst + off), 16, 0, 0);
-#else
         // the 256..768-byte tail in 256-B pieces (one partial 16-B/lane piece instead
         // measured 0.15 ms slower at C2)
         for (; off < cover_bytes; off += 256)
             __builtin_amdgcn_global_load_lds((const void *)(src + off + 4 * lane),
                                              (__attribute__((address_space(3))) void *)(dst + off), 4, 0, 0);
-#endif
     } else {
         for (int off = 0; off < cover_bytes; off += 256) {
             int idx = start + (off >> 2) + lane;
@@ -1391,87 +1373,6 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
         }
     };
 
-    // ---- select build (8-bit rows, a.sel): one unit = one group x kSelPos
-    // positions p (slot s holds position p at element p - lo_s).  Every channel k of the
-    // group is read at its <= 3 candidate offsets once per position - two bytes packed
-    // into one register (bytes 0 and 2), the third into another (byte 4 of the pair) -
-    // and each pair of slots takes its channels' bytes with one v_perm_b32
-    // per channel (selector bytes 0 / 2 / 4, or 12 = zero for a missing channel) into two
-    // 16-bit lanes, summed by v_pk_add_u16 (<= 8 x 255: exact), converted to float32 (the
-    // direct build's exact integer sums, bit for bit) and written to both copies of each
-    // slot where its range covers the position (EXEC-masked lanes at the range ends).
-    // Reads per position and group: 3 G bytes instead of G per slot (C3: ~8 slots).
-    auto build_sel = [&](const i32x4 st) {
-        if constexpr (kDma && EB == 1) {
-            constexpr int US = kSelPos / 64;
-            typedef uint32_t selv_t __attribute__((ext_vector_type(G)));
-            typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-            for (int u = st.z + wave; u < st.w; u += W) {
-                const i32x4 ur = ld_uniform(a.units + u);
-                const int32_t *gr = a.grecs + (size_t)ur.x * a.gstride;
-                const i32x4 gh = ld_uniform(reinterpret_cast<const i32x4 *>(gr));  // slots, count, gs, pair0
-                uint32_t c01[US][G], c1[US][G], c2[US][G];
-#pragma unroll
-                for (int k = 0; k < G; ++k) {
-                    const int32_t ak = ld_uniform(gr + kSelHdr + kSelCand * k);  // candidate 0 (1, 2 follow)
-                    const uint32_t addr = smem_addr + (uint32_t)(ak + ur.y + lane);
-#pragma unroll
-                    for (int u2 = 0; u2 < US; ++u2) {
-                        // three whole-register byte reads: with SRAMECC (gfx950) a d16 load
-                        // zeroes the other half of its VGPR, so candidates 0 and 1 cannot
-                        // be packed by ds_read_u8_d16 + _d16_hi
-                        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(c01[u2][k]) : "v"(addr), "i"(64 * u2) : "memory");
-                        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(c1[u2][k]) : "v"(addr), "i"(64 * u2 + 1) : "memory");
-                        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(c2[u2][k]) : "v"(addr), "i"(64 * u2 + 2) : "memory");
-                    }
-                }
-                asm volatile("s_waitcnt lgkmcnt(0)" : : : "memory");
-#pragma unroll
-                for (int u2 = 0; u2 < US; ++u2)
-#pragma unroll
-                    for (int k = 0; k < G; ++k) {
-                        asm volatile("" : "+v"(c01[u2][k]), "+v"(c1[u2][k]), "+v"(c2[u2][k]));
-                        c01[u2][k] |= c1[u2][k] << 16;  // v_lshl_or_b32: bytes 0 / 2 = candidates 0 / 1
-                    }
-                const int nsl = gh.y;
-                for (int q = 0; q < nsl; q += 2) {
-                    const selv_t sv = ld_uniform(reinterpret_cast<const selv_t *>(a.sels) + gh.w + q / 2);
-                    const meta_t ma = ld_uniform(reinterpret_cast<const meta_t *>(slots + (size_t)(gh.x + q) * MS));
-                    const meta_t mb = ld_uniform(
-                        reinterpret_cast<const meta_t *>(slots + (size_t)(gh.x + min(q + 1, nsl - 1)) * MS));
-#pragma unroll
-                    for (int u2 = 0; u2 < US; ++u2) {
-                        u16x2 acc = {0, 0};
-#pragma unroll
-                        for (int k = 0; k < G; ++k)
-                            acc += __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(c2[u2][k], c01[u2][k], sv[k]));
-                        const float ra = static_cast<float>(acc.x), rb = static_cast<float>(acc.y);
-                        const int P = ur.y + 64 * u2;  // first position of this chunk
-                        auto put = [&](const meta_t &m, float r) {
-                            const int i0 = P - m[4];  // element of lane 0
-                            const int lim = m[5];
-                            if (i0 + 64 <= 0 || i0 >= lim) return;  // the chunk misses the slot
-                            const int i = i0 + lane;
-                            // per-lane ds_write_b32: the chunk starts at any element of the
-                            // slot here (ds_write_addtid_b32 with such an M0 base wrote wrong
-                            // elements on the MI355X: it is only used at 64-element chunk
-                            // starts, as in build_pass)
-                            if (i >= 0 && i < lim) {
-                                float *c0p = reinterpret_cast<float *>(smem + m[1]) + i;
-                                c0p[0] = r;
-                                reinterpret_cast<float *>(reinterpret_cast<unsigned char *>(c0p) + copy_bytes)[-1] = r;
-                            }
-                        };
-                        put(ma, ra);
-                        if (q + 1 < nsl) put(mb, rb);
-                    }
-                }
-            }
-        } else {
-            (void)st;
-        }
-    };
-
     // ---- stage loop.  Scalar metadata is loaded one step ahead (the stage records of k+1
     // and k+2, this wave's first DMA row base, slot record and window records), so the
     // loads' latency overlaps the barrier waits instead of the phases.
@@ -1491,7 +1392,7 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
 #endif
     for (int k = 0; k < ns; ++k) {
         const i32x4 st2 = stage_at(k + 2);
-        const meta_t m0 = a.sel ? meta_t{} : meta_of(st);  // select build: the stage indexes units
+        const meta_t m0 = meta_of(st);
         const rec_t rec0 = ld_uniform(recs + (size_t)st.x * W);
         PU_PHASE(0);
         // This wave's LDS-DMA rows have landed before it arrives at the barrier.  Explicit:
@@ -1503,12 +1404,7 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
         __syncthreads();  // raw rows of stage k landed; every wave left the slot area
         PU_PHASE(1);
         const int vb1 = kDma && k + 1 < ns ? bases_of(st1) : 0;  // lands during the build
-        if (!(skip & 1)) {
-            if (a.sel)
-                build_sel(st);
-            else
-                build(st, m0);
-        }
+        if (!(skip & 1)) build(st, m0);
         PU_PHASE(2);
         __syncthreads();  // slots built; every wave left the raw rows
         PU_PHASE(3);
@@ -1790,13 +1686,6 @@ struct SubHost {
     std::vector<i32x2> tile_stages;
     std::vector<int32_t> slots, base;
     std::vector<uint32_t> recs;
-    // select build (8-bit rows, SubArgs::sel): per (stage, group, chunk of kSelPos
-    // positions) a unit {group record, first position}; per group a record (kSelHdr
-    // header ints, then 3 candidate LDS offsets per channel); per pair of slots G v_perm
-    // selectors
-    std::vector<i32x4> units;
-    std::vector<int32_t> grecs;
-    std::vector<uint32_t> sels;
 };
 
 }  // namespace
@@ -1832,15 +1721,11 @@ struct pu_plan {
     int64_t exec_adds = 0, lds_traffic = 0;  // per launch (measurement: bench.py roofline)
     int64_t nstages = 0;
     int dt_major = 0;  // subband item order (SubArgs::dt_major)
-    int opt_u8_dma = -1, opt_dt_major = -1, opt_build = -1;  // pu_plan_opts (planner inputs)
+    int opt_u8_dma = -1, opt_dt_major = -1;  // pu_plan_opts (planner inputs)
     i32x4 *d_tiles = nullptr, *d_stages = nullptr;
     i32x2 *d_tile_stages = nullptr;
     int32_t *d_slots = nullptr;
     uint32_t *d_recs = nullptr;
-    int sel = 0;  // select build (8-bit rows): stage records index units, not slots
-    i32x4 *d_units = nullptr;
-    int32_t *d_grecs = nullptr;
-    uint32_t *d_sels = nullptr;
     // optional kernel timing: events before the first and after the last launch of
     // each dispatch
     std::vector<hipEvent_t> ev_start, ev_stop;
@@ -1919,11 +1804,6 @@ int launch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
     sa.nitems = (int32_t)nitems;
     sa.base_bits = p->base_bits;
     sa.dt_major = p->dt_major;
-    sa.sel = p->sel;
-    sa.gstride = kSelHdr + kSelCand * G;
-    sa.units = p->d_units;
-    sa.grecs = p->d_grecs;
-    sa.sels = p->d_sels;
     const int64_t nblk = nitems;
     const dim3 grid((unsigned)nblk), block(C::THREADS);
     auto go = [&](auto kern) {
@@ -2005,9 +1885,6 @@ void free_plan(pu_plan *p)
     (void)hipFree(p->d_stages);
     (void)hipFree(p->d_slots);
     (void)hipFree(p->d_recs);
-    (void)hipFree(p->d_units);
-    (void)hipFree(p->d_grecs);
-    (void)hipFree(p->d_sels);
     (void)hipFree(p->d_stamps);
     if (p->h_cert) (void)hipHostFree(p->h_cert);
     delete p;
@@ -2362,32 +2239,6 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     int64_t slot_used = 0, max_stage_chans = 0;
     int64_t adds_tile = 0, lds_tile = 0;  // per time tile, summed over DM tiles
     std::vector<double> tile_cost((size_t)ndt);  // per DM tile: LDS bytes + stage overhead (cost model)
-    // Select build (8-bit rows staged by LDS-DMA, round 4): the slots of a group share
-    // their channels' rows at a few relative offsets each (the group's distinct v_k per
-    // channel: 1-3 at C3), so a wave reads each (channel, offset) byte once per position
-    // and forms every slot of the group by byte selects (v_perm_b32) and packed 16-bit
-    // adds (two slots per register), instead of G byte reads per slot and position.
-    // Eligible when every channel of every group has <= kSelCand distinct offsets.
-    bool sel = dma8 && p->opt_build > 0;  // opt-in until measured faster
-    for (int t = 0; sel && t < ndt; ++t)
-        for (int gg = 0; sel && gg < ngroups; ++gg) {
-            const int64_t c0 = (int64_t)gg * G;
-            const int gs = (int)std::min<int64_t>(G, nchan - c0);
-            const auto &sls = tslots[(size_t)t * ngroups + gg];
-            for (int k = 1; sel && k < gs; ++k) {
-                int64_t vmin = INT64_MAX, vmax = INT64_MIN;
-                for (const auto &sl : sls) {
-                    const int64_t v = S(sl.d0, c0 + k) - S(sl.d0, c0);
-                    vmin = std::min(vmin, v);
-                    vmax = std::max(vmax, v);
-                }
-                sel = vmax - vmin < kSelCand;
-            }
-        }
-    const int gstride = kSelHdr + kSelCand * G;
-    std::vector<i32x4> units;
-    std::vector<int32_t> grecs;
-    std::vector<uint32_t> sels;
     for (int t = 0; t < ndt; ++t) {
         const int64_t lds_before = lds_tile;
         const int64_t cb = copy_of(span_t[t]);
@@ -2435,77 +2286,19 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
                 prev_slots = u * 2 * cb;
             }
             int g_end = g;
-            const int32_t u_begin = (int32_t)units.size();
             while (g_end < g_stop) {
                 const int64_t c0 = (int64_t)g_end * G;
                 const int gs = (int)std::min<int64_t>(G, nchan - c0);
                 const auto &sls = tslots[(size_t)t * ngroups + g_end];
                 slot_local[g_end] = used;
-                if (sel) {
-                    // group record: slots, candidate offsets per channel; slot pairs' selectors;
-                    // units over the union of the slots' position ranges
-                    const int32_t grec = (int32_t)(grecs.size() / gstride);
-                    const int64_t nsl = (int64_t)sls.size();
-                    grecs.push_back((int32_t)(slotmeta.size() / ms));
-                    grecs.push_back((int32_t)nsl);
-                    grecs.push_back(gs);
-                    grecs.push_back((int32_t)(sels.size() / G));
-                    // candidates of channel k: offsets vmin_k + j, j < kSelCand (slot index j =
-                    // its v_k - vmin_k; v_perm byte 2 j: c0 | c1 << 16 in one register, c2 in
-                    // the other)
-                    std::vector<int64_t> vmin((size_t)G, INT64_MAX);
-                    for (const auto &sl : sls)
-                        for (int k = 0; k < gs; ++k)
-                            vmin[k] = std::min(vmin[k], S(sl.d0, c0 + k) - S(sl.d0, c0));
-                    for (int k = 0; k < G; ++k)
-                        for (int j = 0; j < kSelCand; ++j) {
-                            int64_t a = 0;  // missing channel: never selected
-                            if (k < gs)
-                                a = raw_top_f(g, g_stop) + (chans + k) * raw_stride - smin[c0 + k] +
-                                    (base_of(smin[c0 + k]) & 3) + vmin[k] + j;
-                            grecs.push_back((int32_t)a);
-                        }
-                    for (int64_t si = 0; si < nsl; si += 2)
-                        for (int k = 0; k < G; ++k) {
-                            uint32_t w = 0x0C0C0C0Cu;  // v_perm: 12 selects a zero byte
-                            if (k < gs) {
-                                const int64_t ia = S(sls[si].d0, c0 + k) - S(sls[si].d0, c0) - vmin[k];
-                                w = (w & ~0xffu) | (uint32_t)(2 * ia);
-                                if (si + 1 < nsl) {
-                                    const int64_t ib = S(sls[si + 1].d0, c0 + k) - S(sls[si + 1].d0, c0) - vmin[k];
-                                    w = (w & ~0xff0000u) | ((uint32_t)(2 * ib) << 16);
-                                }
-                            }
-                            sels.push_back(w);
-                        }
-                    int64_t pmin = INT64_MAX, pmax = INT64_MIN;
-                    for (const auto &sl : sls) {
-                        const int64_t len = TT + (sl.hi - sl.lo) + 1;
-                        pmin = std::min(pmin, sl.lo);
-                        pmax = std::max(pmax, sl.lo + (len + 63) / 64 * 64);
-                    }
-                    for (int64_t p0 = pmin; p0 < pmax; p0 += kSelPos) {
-                        units.push_back(i32x4{grec, (int32_t)p0, 0, 0});
-                        const int64_t m = std::min<int64_t>(kSelPos, pmax - p0);
-                        lds_tile += (m + 63) / 64 * 64 * (kSelCand * gs + 8 * nsl);  // reads + 2 writes per slot
-                    }
-                }
                 for (const auto &sl : sls) {
                     const int64_t len = TT + (sl.hi - sl.lo) + 1;
                     adds_tile += len * gs;
-                    if (!sel) lds_tile += ((len + 63) / 64 * 64) * (dma ? eb * G + 8 : 8);  // build reads + 2 writes
+                    lds_tile += ((len + 63) / 64 * 64) * (dma ? eb * G + 8 : 8);  // build reads + 2 writes
                     slotmeta.push_back((int32_t)len);
                     slotmeta.push_back((int32_t)(zr + used * 2 * cb));
                     slotmeta.push_back((int32_t)c0);
                     slotmeta.push_back(gs);
-                    if (sel) {
-                        // select build: the slot's first position and written length
-                        slotmeta.push_back((int32_t)sl.lo);
-                        slotmeta.push_back((int32_t)((len + 63) / 64 * 64));
-                        for (int k = 0; k < ms - 6; ++k) slotmeta.push_back(0);
-                        ++used;
-                        continue;
-                    }
                     for (int k = 0; k < ms - 4; ++k) {
                         int64_t src = dma && k < G ? zero_row_f : 0;  // missing channel: zero row
                         if (k < gs) {
@@ -2526,10 +2319,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
                 chans += gs;
                 ++g_end;
             }
-            if (sel)
-                stages.push_back(i32x4{g, g_end, u_begin, (int32_t)units.size()});
-            else
-                stages.push_back(i32x4{g, g_end, s_begin, (int32_t)(slotmeta.size() / ms)});
+            stages.push_back(i32x4{g, g_end, s_begin, (int32_t)(slotmeta.size() / ms)});
             tile_stages[t][1]++;
             if (dma) lds_tile += chans * ((row_len * eb + 255) / 256 * 256);  // DMA writes
             slot_used = std::max(slot_used, zr + used * 2 * cb);
@@ -2627,12 +2417,6 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     h.slots = std::move(slotmeta);
     h.recs = std::move(rec);
     h.base = dma ? std::move(base) : std::vector<int32_t>();
-    p->sel = sel ? 1 : 0;
-    if (sel) {
-        h.units = std::move(units);
-        h.grecs = std::move(grecs);
-        h.sels = std::move(sels);
-    }
     return PU_OK;
 }
 
@@ -2646,9 +2430,6 @@ int upload_sub(pu_plan *p)
     if (!rc) rc = upload(&p->d_slots, h.slots);
     if (!rc) rc = upload(&p->d_recs, h.recs);
     if (!rc && !h.base.empty()) rc = upload(&p->d_base, h.base);
-    if (!rc && p->sel) rc = upload(&p->d_units, h.units);
-    if (!rc && p->sel) rc = upload(&p->d_grecs, h.grecs);
-    if (!rc && p->sel) rc = upload(&p->d_sels, h.sels);
     h = SubHost{};
     return rc;
 }
@@ -2667,7 +2448,6 @@ void reset_tables(pu_plan *p)
     keep.ntt = p->ntt;
     keep.opt_u8_dma = p->opt_u8_dma;
     keep.opt_dt_major = p->opt_dt_major;
-    keep.opt_build = p->opt_build;
     (void)hipFree(p->d_first);
     (void)hipFree(p->d_count);
     (void)hipFree(p->d_rowlen);
@@ -2678,9 +2458,6 @@ void reset_tables(pu_plan *p)
     (void)hipFree(p->d_stages);
     (void)hipFree(p->d_slots);
     (void)hipFree(p->d_recs);
-    (void)hipFree(p->d_units);
-    (void)hipFree(p->d_grecs);
-    (void)hipFree(p->d_sels);
     *p = keep;
 }
 
@@ -2852,9 +2629,8 @@ int pu_plan_create_ex(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t 
     PU_REQUIRE(opts->shape >= -1 && opts->shape <= 2, "pu_plan_create_ex: shape %d not in {-1, 0, 1, 2}", opts->shape);
     PU_REQUIRE(opts->lds_budget_kb == 0 || (opts->lds_budget_kb >= 8 && opts->lds_budget_kb <= 160),
                "pu_plan_create_ex: lds_budget_kb %d not 0 or in [8, 160]", opts->lds_budget_kb);
-    PU_REQUIRE(opts->u8_dma >= -1 && opts->u8_dma <= 1 && opts->dt_major >= -1 && opts->dt_major <= 1 &&
-                   opts->build >= -1 && opts->build <= 1,
-               "pu_plan_create_ex: u8_dma / dt_major / build must be -1, 0 or 1");
+    PU_REQUIRE(opts->u8_dma >= -1 && opts->u8_dma <= 1 && opts->dt_major >= -1 && opts->dt_major <= 1,
+               "pu_plan_create_ex: u8_dma / dt_major must be -1, 0 or 1");
     *out = nullptr;
     const int v = pick_variant(dtype, acc);
     PU_REQUIRE(v >= 0, "pu_plan_create: unsupported dtype %d", dtype);
@@ -2882,7 +2658,6 @@ int pu_plan_create_ex(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t 
     p->ntt = (int)((n + p->TT - 1) / p->TT);
     p->opt_u8_dma = opts->u8_dma < 0 ? 1 : opts->u8_dma;
     p->opt_dt_major = opts->dt_major;
-    p->opt_build = pu::knob("PU_SEL_BUILD", opts->build);
 
     // subband workgroup shape: 0 = wide (1 WG/CU), 1 = pair (2 WGs/CU), 2 = tall (256
     // trials x 256 samples, 1 WG/CU); -1 = the cost model's choice among wide and tall.
@@ -2931,7 +2706,6 @@ int pu_plan_create_ex(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t 
             q->ntt = p->ntt;
             q->opt_u8_dma = p->opt_u8_dma;
             q->opt_dt_major = p->opt_dt_major;
-            q->opt_build = p->opt_build;
             return q;
         };
         // Round 3: the tall shape (256 trials x 256 samples) competes too, with G = 4 and 8.
@@ -2993,7 +2767,6 @@ int pu_plan_create_grouped(pu_plan **out, int dtype, int acc, int64_t nchan, int
     o.shape = -1;
     o.u8_dma = -1;
     o.dt_major = -1;
-    o.build = -1;
     return pu_plan_create_ex(out, dtype, acc, nchan, n, shifts, ndm, &o);
 }
 
@@ -3068,7 +2841,7 @@ int pu_plan_info(const pu_plan *p, int64_t *info, int n)
                          p->row_stride, (int64_t)p->lds_bytes, kVariants[p->variant].acc_f64, p->max_spread,
                          p->group, p->nslots_total, p->nstages, (int64_t)p->slot_bytes, p->raw_stride,
                          p->exec_adds, p->lds_traffic, p->cert_rechecked, p->cert_nan, p->cert_why[0],
-                         p->cert_why[1], p->cert_why[2], p->cert_us, p->sel};
+                         p->cert_why[1], p->cert_why[2], p->cert_us};
     const int m = std::min<int>(n, (int)(sizeof v / sizeof v[0]));
     for (int k = 0; k < m; ++k) info[k] = v[k];
     return m;

@@ -56,6 +56,7 @@ SIGNATURES = {
     "pu_zero_columns": (_i32, [_vp, _i64, _i64, _vp, _i64, _vp]),
     "pu_cut_outliers_workspace_bytes": (_sz, [_i64]),
     "pu_cut_outliers": (_i32, [_vp, _i64, _vp, _i64, _i64, _vp, _vp, _sz, _vp]),
+    "pu_cut_outliers_exact": (_i32, [_vp, _i64, _vp, _i64, _i64, _vp, _vp, _sz, _vp]),
     "pu_rebin_time": (_i32, [_vp, _i32, _i64, _i64, _i64, _i64, _vp, _vp]),
     "pu_rebin_chan": (_i32, [_vp, _i32, _i64, _i64, _i64, _i64, _vp, _vp]),
     "pu_roll_rows": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp]),
@@ -68,7 +69,7 @@ SIGNATURES = {
 INFO_FIELDS = ("ndm", "dm_tiles", "time_tiles", "trials_per_tile", "time_tile", "chans_per_step",
                "row_stride", "lds_bytes", "acc_is_f64", "max_spread", "group", "slots", "stages",
                "slot_bytes", "raw_stride", "exec_adds", "lds_traffic", "cert_rechecked", "cert_nan", "cert_std", "cert_sign",
-               "cert_tie", "cert_us", "select_build")
+               "cert_tie", "cert_us")
 
 
 class HipBackendError(RuntimeError):
@@ -78,8 +79,7 @@ class HipBackendError(RuntimeError):
 class PlanOpts(ctypes.Structure):
     """``pu_plan_opts`` (include/pulsarutils_hip.h): the planner's explicit options."""
     _fields_ = [("group", ctypes.c_int32), ("shape", ctypes.c_int32), ("lds_budget_kb", ctypes.c_int32),
-                ("u8_dma", ctypes.c_int32), ("dt_major", ctypes.c_int32), ("build", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 2)]
+                ("u8_dma", ctypes.c_int32), ("dt_major", ctypes.c_int32), ("reserved", ctypes.c_int32 * 3)]
 
 
 SHAPES = {"wide": 0, "pair": 1, "tall": 2}
@@ -127,8 +127,16 @@ def lib():
                     raise HipBackendError(
                         f"pulsarutils: HIP library not found at {_LIB_PATH}; build it with "
                         "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+                # PyTorch first: its wheel bundles its own libamdhip64.so.7 / HSA runtime.
+                # Loaded after ours (RUNPATH /opt/rocm), the process would hold TWO HIP and
+                # HSA runtimes, and the second to open the GPU finds "no ROCm-capable
+                # device" (seen on the MI355X box when the first call was shift_table).
+                # With torch loaded, our DT_NEEDED libamdhip64.so.7 resolves to its copy.
+                torch()
                 L = ctypes.CDLL(_LIB_PATH)
                 for name, (res, args) in SIGNATURES.items():
+                    if "PULSARUTILS_HIP_LIB" in os.environ and not hasattr(L, name):
+                        continue  # an older build loaded for an A/B run (scripts/ab_lib.sh)
                     fn = getattr(L, name)
                     fn.restype = res
                     fn.argtypes = args
@@ -208,15 +216,14 @@ class Plan:
     """Owning wrapper of a ``pu_plan`` (dedispersion tiling + device metadata)."""
 
     def __init__(self, dtype_code_, acc, nchan, nsamples, shifts, group=0, shape=None, lds_budget_kb=0,
-                 u8_dma=None, dt_major=None, select_build=None):
+                 u8_dma=None, dt_major=None):
         """``group``: channels summed per group row (0 = library default, 1 = channel
         mode, 2/4/8); float64 accumulation always uses channel mode.  ``shape``: subband
         workgroup shape ("wide", "pair", "tall" or 0/1/2; None = the cost model's choice);
         ``lds_budget_kb``: LDS per workgroup (0 = default); ``u8_dma``: False builds 8-bit
         slots from global memory instead of LDS-DMA'd rows; ``dt_major``: work-item order
-        (None = automatic); ``select_build``: False keeps the direct slot build of 8-bit
-        plans (None = the select build where eligible).  These are the
-        planner's only inputs (pu_plan_create_ex): the library reads no environment."""
+        (None = automatic).  These are the planner's only inputs (pu_plan_create_ex): the
+        library reads no environment."""
         require_gpu()
         sh = np.ascontiguousarray(shifts, dtype=np.int64)
         if sh.ndim != 2 or sh.shape[1] != int(nchan):
@@ -224,8 +231,7 @@ class Plan:
         ndm = sh.shape[0]
         opts = PlanOpts(group=int(group), shape=-1 if shape is None else int(SHAPES.get(shape, shape)),
                         lds_budget_kb=int(lds_budget_kb), u8_dma=-1 if u8_dma is None else int(bool(u8_dma)),
-                        dt_major=-1 if dt_major is None else int(bool(dt_major)),
-                        build=-1 if select_build is None else int(bool(select_build)))
+                        dt_major=-1 if dt_major is None else int(bool(dt_major)))
         h = ctypes.c_void_p()
         check(lib().pu_plan_create_ex(ctypes.byref(h), dtype_code_, acc, nchan, nsamples,
                                       sh.ctypes.data_as(ctypes.c_void_p), ndm, ctypes.byref(opts)),

@@ -197,8 +197,9 @@ def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=
     rows in order) -> gaussian_filter (GPU, scipy's order) -> median (GPU radix
     select) -> factor
     -> per-channel mean of x*factor (numpy pairwise order) -> (x*f - mu)/mu with bad
-    channels zeroed [+ its column mean] -> host uniform_filter1d(16) thresholds ->
-    zero the bad time bins.
+    channels zeroed [+ its column mean] -> uniform_filter1d(16) thresholds on the
+    device (certified; scipy's own running sum on the device when a decision is
+    ambiguous) -> zero the bad time bins.  No host synchronisation for n >= 64.
 
     ``zero_dm=True`` (opt-in; the reference has no counterpart, see renormalize_data)
     also subtracts, per time bin, the mean of the normalised good channels, fused into
@@ -243,27 +244,15 @@ def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=
                    "pu_renorm_apply")
     bad_bins = None
     if cut_outliers and n >= 64:
-        # device path: certified decisions (pu_cut_outliers); the flag word says whether
-        # every decision was provably the reference's
+        # device path (pu_cut_outliers): certified decisions, and the reference's own
+        # arithmetic on the device for the rare ambiguous / NaN case - no host round trip
         ws = t.empty(lib.pu_cut_outliers_workspace_bytes(n), dtype=t.uint8, device=dev)
         mask = t.empty(n, dtype=t.uint8, device=dev)
         _hip.check(lib.pu_cut_outliers(_hip.ptr(col), n, _hip.ptr(out), nchan, out.stride(0), _hip.ptr(mask),
                                        _hip.ptr(ws), ws.numel(), s), "pu_cut_outliers")
-        flag = int(ws[:4].view(t.int32).item())
-        if flag == 0:
-            return out, mask.view(t.bool)
-        # ambiguous (a window mean within rounding distance of a threshold) or NaN: redo
-        # the apply pass (the plane may already have zeroed columns) and run scipy's own
-        # running-sum filter on the host, as the reference does
-        if zero_dm:
-            _hip.check(lib.pu_renorm_apply_zero_dm(_hip.ptr(x), code, nchan, n, x.stride(0), _hip.ptr(factor),
-                                                   _hip.ptr(spec), _hip.ptr(bad), ngood, _hip.ptr(out),
-                                                   out.stride(0), _hip.ptr(col), s), "pu_renorm_apply_zero_dm")
-        else:
-            _hip.check(lib.pu_renorm_apply(_hip.ptr(x), code, nchan, n, x.stride(0), _hip.ptr(factor),
-                                           _hip.ptr(spec), _hip.ptr(bad), _hip.ptr(out), out.stride(0),
-                                           _hip.ptr(col), s), "pu_renorm_apply")
+        return out, mask.view(t.bool)
     if cut_outliers:
+        # n < 64: scipy on the host, as the reference does
         lc2 = _host(col)
         window = 16  # only the last window of the reference loop (range(0, 5)) survives
         lc_rebin = uniform_filter1d(lc2, window)

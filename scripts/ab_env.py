@@ -34,17 +34,14 @@ for v in variants:
     saved = {k: os.environ.get(k) for k in kv}
     os.environ.update(kv)
     acc = {"native": _hip.PU_ACC_NATIVE, "f32": _hip.PU_ACC_F32, "f64": _hip.PU_ACC_F64}[os.environ.get("AB_ACC", "native")]
-    # AB_SELECT=1: the 8-bit select build (libraries from round 4 on; older ones reject it)
-    extra = {"select_build": True} if os.environ.get("AB_SELECT") == "1" else {}
-    plans[v] = _hip.Plan(_hip.dtype_code(x.dtype), acc, cfg.nchan, cfg.nsamples, sh, **extra)
+    plans[v] = _hip.Plan(_hip.dtype_code(x.dtype), acc, cfg.nchan, cfg.nsamples, sh)
     for k, val in saved.items():
         if val is None:
             os.environ.pop(k, None)
         else:
             os.environ[k] = val
     print("variant", v, json.dumps({k: plans[v].info[k] for k in ("group", "stages", "dm_tiles", "time_tiles", "lds_traffic", "lds_bytes",
-                                                                    "slot_bytes", "raw_stride")} | {"select_build": plans[v].info.get("select_build")}),
-          flush=True)
+                                                                    "slot_bytes", "raw_stride")}), flush=True)
 ws = torch.empty(max(p.workspace_bytes for p in plans.values()), dtype=torch.uint8, device=x.device)
 res = {v: [] for v in plans}
 ref = None

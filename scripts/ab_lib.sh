@@ -6,8 +6,6 @@ A=${A:-head}; B=${B:-new}; CFG=${CFG:-C3}; TRIALS=${TRIALS:-625}; ROUNDS=${ROUND
 for r in $(seq 1 "$ROUNDS"); do
   for v in "$A" "$B"; do
     echo "== round $r lib $v"
-    # SEL_LIBS="new ...": those libraries plan with the select build (scripts/ab_env.py)
-    if [[ " ${SEL_LIBS:-} " == *" $v "* ]]; then export AB_SELECT=1; else unset AB_SELECT; fi
     PULSARUTILS_HIP_LIB=ab/lib_$v.so PU_AB="AB_LIB=$v" PU_TRIALS=$TRIALS \
       timeout -k 10 240 python -u scripts/ab_env.py "$CFG" 2
   done

@@ -38,3 +38,5 @@ timed(lambda: y.fill_(1.0), y.numel() * 8, "fill f64")
 timed(lambda: y.copy_(x32), x32.numel() * 12, "copy f32->f64")
 timed(lambda: y.copy_(x8), x8.numel() * 9, "copy u8->f64")
 timed(lambda: x32.sum(dtype=torch.float32), x32.numel() * 4, "sum f32 (read)")
+timed(lambda: x32.sum(dim=0), x32.numel() * 4, "column sums f32 (read, axis 0)")
+timed(lambda: x32.sum(dim=1), x32.numel() * 4, "row sums f32 (read, axis 1)")

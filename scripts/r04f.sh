@@ -14,6 +14,8 @@ timeout -k 10 900 python -u -m pytest tests -v -m gpu -x --timeout 300 --timeout
 SEL_LIBS=new A=head B=new CFG=C3 TRIALS=625 ROUNDS=2 timeout -k 10 400 bash scripts/ab_lib.sh > $OUT/ab_c3_625.log 2>&1 || exit $?
 SEL_LIBS=new A=head B=new CFG=C3 TRIALS=0 ROUNDS=1 timeout -k 10 400 bash scripts/ab_lib.sh > $OUT/ab_c3_5000.log 2>&1 || exit $?
 echo done > $OUT/status.txt
-A=new B=tail CFG=C2 TRIALS=1000 ROUNDS=2 timeout -k 10 300 bash scripts/ab_lib.sh > $OUT/ab_c2_tail.log 2>&1 || exit $?
-A=new B=tail CFG=C5 TRIALS=0 ROUNDS=2 timeout -k 10 300 bash scripts/ab_lib.sh > $OUT/ab_c5_tail.log 2>&1 || exit $?
+A=new B=tail CFG=C2 TRIALS=1000 ROUNDS=1 timeout -k 10 300 bash scripts/ab_lib.sh > $OUT/ab_c2_tail.log 2>&1 || exit $?
+A=new B=tail CFG=C5 TRIALS=0 ROUNDS=1 timeout -k 10 300 bash scripts/ab_lib.sh > $OUT/ab_c5_tail.log 2>&1 || exit $?
 echo done2 > $OUT/status2.txt
+timeout -k 10 400 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-c3-strong > $OUT/bench.json 2> $OUT/bench.err || exit $?
+echo done3 > $OUT/status3.txt

@@ -74,3 +74,22 @@ def test_production_library_reads_no_tuning_environment():
     for knob in (b"PU_SUB_SHAPE", b"PU_GROUP", b"PU_LDS_BUDGET_KB", b"PU_U8_DMA", b"PU_DT_MAJOR", b"PU_CLEAN_BATCH",
                  b"PU_APPLY_BATCH", b"PU_MEDIAN_GRID", b"PU_COLSEG", b"PU_SUB_SKIP", b"PU_DMA_WAVES"):
         assert knob not in blob, knob
+
+
+def test_one_hip_runtime_when_the_library_loads_first():
+    """A process whose first pulsarutils call is host-only (shift_table) must still hold ONE
+    HIP and HSA runtime: lib() imports torch before dlopen, so the library's
+    libamdhip64.so.7 resolves to the copy PyTorch bundles (two runtimes made the library's
+    hipMalloc fail with "no ROCm-capable device" on the MI355X box)."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from pulsarutils import _hip\n"
+            "_hip.shift_table(8, [1.0], 1400.0, 100.0, 1e-4)\n"
+            "import torch\n"
+            "maps = open('/proc/self/maps').read().splitlines()\n"
+            "libs = {l.split()[-1] for l in maps if 'libamdhip64' in l or 'libhsa-runtime64' in l}\n"
+            "print(len(libs))\n") % os.path.join(REPO, "radio-pulsar-utils_amd")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip().splitlines()[-1] == "2", out.stdout  # one libamdhip64 + one libhsa-runtime64

@@ -160,6 +160,54 @@ def test_cut_outliers_device_certified(gpu):
     torch.cuda.synchronize()
 
 
+def test_cut_outliers_exact_path_on_device(gpu):
+    """The exact path of pu_cut_outliers (round 4: scipy's running-sum uniform_filter1d
+    and numpy's std order in one workgroup, instead of a host round trip) gives the
+    reference's mask bit for bit - forced through pu_cut_outliers_exact on spiky light
+    curves whose bins sit within rounding of the thresholds too, and reached through the
+    flag by a NaN - and zeroes exactly the bad columns of the plane."""
+    import torch
+    from scipy.ndimage import uniform_filter1d
+    from pulsarutils import _hip
+    lib = _hip.lib()
+    rng = np.random.default_rng(29)
+    for n in (64, 1000, 70001, 262144):
+        lc = rng.standard_normal(n) * 0.01
+        lc[rng.integers(0, n, 9)] += 0.3
+        reb = uniform_filter1d(lc, 16)
+        sd = np.std(reb[::16])
+        lc[n // 2:n // 2 + 16] += (5 * sd - reb[n // 2 + 8])  # a window mean at the threshold
+        reb = uniform_filter1d(lc, 16)
+        sd = np.std(reb[::16])
+        want = (reb > 5 * sd) | (reb < -3 * sd)
+        nrows = 3
+        for fn in (lib.pu_cut_outliers_exact, lib.pu_cut_outliers):
+            out = torch.ones((nrows, n), dtype=torch.float64, device="cuda")
+            col = torch.from_numpy(lc).cuda()
+            ws = torch.empty(lib.pu_cut_outliers_workspace_bytes(n), dtype=torch.uint8, device="cuda")
+            mask = torch.empty(n, dtype=torch.uint8, device="cuda")
+            _hip.check(fn(_hip.ptr(col), n, _hip.ptr(out), nrows, out.stride(0), _hip.ptr(mask), _hip.ptr(ws),
+                          ws.numel(), _hip.stream_ptr()), "cut_outliers")
+            got = mask.cpu().numpy().astype(bool)
+            np.testing.assert_array_equal(got, want, err_msg=f"n {n} {fn.__name__}")
+            o = out.cpu().numpy()
+            assert not o[:, want].any() and (o[:, ~want] == 1.0).all()
+            assert int(ws[4:8].view(torch.int32).item()) == int(want.sum())
+    # NaN: the flag routes to the exact path; numpy's comparisons with NaN are False
+    lc = rng.standard_normal(5000)
+    lc[1234] = np.nan
+    out = torch.ones((2, 5000), dtype=torch.float64, device="cuda")
+    col = torch.from_numpy(lc).cuda()
+    ws = torch.empty(lib.pu_cut_outliers_workspace_bytes(5000), dtype=torch.uint8, device="cuda")
+    mask = torch.empty(5000, dtype=torch.uint8, device="cuda")
+    _hip.check(lib.pu_cut_outliers(_hip.ptr(col), 5000, _hip.ptr(out), 2, 5000, _hip.ptr(mask), _hip.ptr(ws),
+                                   ws.numel(), _hip.stream_ptr()), "pu_cut_outliers")
+    reb = uniform_filter1d(lc, 16)
+    sd = np.std(reb[::16])
+    np.testing.assert_array_equal(mask.cpu().numpy().astype(bool), (reb > 5 * sd) | (reb < -3 * sd))
+    assert int(ws[0:4].view(torch.int32).item()) == 1
+
+
 def test_zero_dm_small_cases(gpu):
     """Ragged sizes, all channels bad, no channel bad."""
     rng = np.random.default_rng(13)

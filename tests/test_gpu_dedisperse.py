@@ -534,47 +534,3 @@ def test_default_group_ragged_vs_oracle(gpu, dt):
         pf = _plane(x, sh, "native", forced)
         if dt == "u8":
             np.testing.assert_array_equal(pf, plane)
-
-
-@pytest.mark.parametrize("group", [4, 8])
-@pytest.mark.parametrize("shape", [0, 1, 2])
-@pytest.mark.parametrize("nchan", [1030, 1024])
-def test_select_build_equals_direct(gpu, shape, group, nchan):
-    """The select build of 8-bit slots (round 4: each channel read once per position at its
-    <= 3 candidate offsets, slots formed by v_perm byte selects and packed 16-bit adds)
-    gives the direct build's plane and search bit for bit, and the oracle's series; wide /
-    pair / tall shapes, G = 4 and 8, a partial last group (130 % G != 0), row misalignments.
-    The grids are narrow enough for every group to be eligible (select_build == 1)."""
-    c = CONFIGS["C3"]
-    rng = np.random.default_rng(nchan + 7 * group + shape)
-    n = 8192
-    x = (rng.random((nchan, n)) * 255).astype(np.uint8)
-    dms = np.linspace(0.0, 12.0, 300)
-    sh = _hip.shift_table(nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
-    sel = _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, nchan, n, sh, group=group, shape=shape, select_build=True)
-    direct = _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, nchan, n, sh, group=group, shape=shape, select_build=False)
-    assert sel.info["select_build"] == 1 and direct.info["select_build"] == 0, sel.info
-    xd = _hip.to_device(x)
-    a, b = sel.dedisperse(xd).cpu().numpy(), direct.dedisperse(xd).cpu().numpy()
-    np.testing.assert_array_equal(a, b)
-    for k in range(0, 300, 37):
-        np.testing.assert_array_equal(a[k].astype(np.float64), oracle.dedisperse(x, sh[k]))
-    for u, v in zip(sel.search(xd), direct.search(xd)):
-        np.testing.assert_array_equal(u.cpu().numpy(), v.cpu().numpy())
-
-
-def test_select_build_ineligible_grid_falls_back(gpu):
-    """A grid whose slots' relative offsets spread over more than 3 samples in some group
-    (130 channels: wide channel spacing) keeps the direct build (select_build == 0) and
-    still matches the oracle."""
-    c = CONFIGS["C3"]
-    rng = np.random.default_rng(5)
-    nchan, n = 130, 8192
-    x = (rng.random((nchan, n)) * 255).astype(np.uint8)
-    dms = np.linspace(0.0, 12.0, 300)
-    sh = _hip.shift_table(nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
-    plan = _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, nchan, n, sh, group=8, shape=2, select_build=True)
-    assert plan.info["select_build"] == 0
-    plane = plan.dedisperse(_hip.to_device(x)).cpu().numpy()
-    for k in range(0, 300, 61):
-        np.testing.assert_array_equal(plane[k].astype(np.float64), oracle.dedisperse(x, sh[k]))

@@ -189,3 +189,22 @@ def test_oracle_degenerate_trials_bitexact(golden, case):
     got = oracle.search(x, dms, f0, bw, ts, nthreads=8)
     for g, r in zip(got, ref):
         np.testing.assert_array_equal(g, r)
+
+
+def test_cut_outliers_exact_restatement():
+    """The order outlier_exact_kernel follows (the device's exact cut_outliers path,
+    round 4) is scipy's and numpy's bit for bit: uniform_filter1d(lc, 16) as scipy's
+    running sum, np.std(lc_rebin[::16]) in add.reduce order - spiky light curves,
+    lengths 64 .. 2^18 + 1, a NaN (propagates through the running sum)."""
+    from scipy.ndimage import uniform_filter1d
+    rng = np.random.default_rng(23)
+    for n in (64, 100, 4097, 70001, 262145):
+        lc = rng.standard_normal(n) * 3.0 + 0.5
+        lc[rng.integers(0, n, 7)] += 40.0
+        got = co.uniform_filter1d_running(lc)
+        want = uniform_filter1d(lc, 16)
+        np.testing.assert_array_equal(got, want)
+        assert co.std_numpy_order(want[::16]) == np.std(want[::16])
+    lc = rng.standard_normal(500)
+    lc[300] = np.nan
+    np.testing.assert_array_equal(co.uniform_filter1d_running(lc), uniform_filter1d(lc, 16))
