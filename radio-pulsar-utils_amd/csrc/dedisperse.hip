@@ -1297,26 +1297,44 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
     // C2, 20.2 vs 18.4 ms).
     auto build_pass = [&](auto upc, const meta_t &m, int gs, int i0, int lim) {
         constexpr int UP = decltype(upc)::value;
-        float v[UP][G];
         auto at = [&](int u) { return i0 + 64 * u + lane; };
-        if (kDma || gs == G) {  // branch-free, all G x UP reads in flight (DMA mode: a
-                                // partial group's missing channels read the zero row)
-#pragma unroll
-            for (int u = 0; u < UP; ++u)
-#pragma unroll
-                for (int q = 0; q < G; ++q) v[u][q] = load(m, q, at(u));
-        } else {        // the last, partial group of a band
-#pragma unroll
-            for (int u = 0; u < UP; ++u)
-#pragma unroll
-                for (int q = 0; q < G; ++q) v[u][q] = q < gs ? load(m, q, at(u)) : 0.0f;
-        }
         float r[UP];
+        if constexpr (kDma && EB == 1) {
+            // 8-bit rows: the bytes summed as integers (v_add3_u32), one convert per element
+            // - the same float32 value as the float sum (every partial sum < 2^24 is exact),
+            // a third of the VALU work of a convert + add per byte
+            uint32_t w[UP][G];
 #pragma unroll
-        for (int u = 0; u < UP; ++u) {
-            r[u] = 0.0f;
+            for (int u = 0; u < UP; ++u)
 #pragma unroll
-            for (int q = 0; q < G; ++q) r[u] += v[u][q];
+                for (int q = 0; q < G; ++q) w[u][q] = raw_lds8[m[4 + q] + at(u)];  // ds_read_u8
+#pragma unroll
+            for (int u = 0; u < UP; ++u) {
+                uint32_t s = 0;
+#pragma unroll
+                for (int q = 0; q < G; ++q) s += w[u][q];
+                r[u] = static_cast<float>(s);
+            }
+        } else {
+            float v[UP][G];
+            if (kDma || gs == G) {  // branch-free, all G x UP reads in flight (DMA mode: a
+                                    // partial group's missing channels read the zero row)
+#pragma unroll
+                for (int u = 0; u < UP; ++u)
+#pragma unroll
+                    for (int q = 0; q < G; ++q) v[u][q] = load(m, q, at(u));
+            } else {        // the last, partial group of a band
+#pragma unroll
+                for (int u = 0; u < UP; ++u)
+#pragma unroll
+                    for (int q = 0; q < G; ++q) v[u][q] = q < gs ? load(m, q, at(u)) : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < UP; ++u) {
+                r[u] = 0.0f;
+#pragma unroll
+                for (int q = 0; q < G; ++q) r[u] += v[u][q];
+            }
         }
         // all sums before the first (chunk-uniform) write branch: keeps every read
         // of the pass in flight together

@@ -27,7 +27,18 @@ def consumer(op, code):
 
 
 def main(path):
-    lines = [ln.split(";")[0].strip() for ln in open(path).read().splitlines()]
+    raw = open(path).read().splitlines()
+    lines = [ln.split(";")[0].strip() for ln in raw]
+    # inline-asm regions (the build's own M0 writes sit between ;;#ASMSTART / ;;#ASMEND;
+    # a compiler-written "s_mov_b32 m0 / s_nop 0" pair outside them is the compiler's)
+    in_asm, asm = False, []
+    for ln in raw:
+        t = ln.strip()
+        if t.startswith(";;#ASMSTART"):
+            in_asm = True
+        elif t.startswith(";;#ASMEND"):
+            in_asm = False
+        asm.append(in_asm)
     text_kernels = 0
     bad = total = 0
     i = 0
@@ -50,8 +61,7 @@ def main(path):
             op = code.split()[0]
             dst = code.split(",")[0]
             if op.startswith("s_") and re.search(r"\bm0\b", dst) and op not in ("s_sendmsg", "s_sendmsghalt"):
-                nxt = lines[i] if i < len(lines) else ""
-                state = "ours" if (op == "s_mov_b32" and nxt.startswith("s_nop 0")) else "cc"
+                state = "ours" if asm[i - 1] else "cc"
                 continue
             if op.startswith("ds_write_addtid"):
                 # the build's own stores (inline asm after its own M0 write; their guarded
