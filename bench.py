@@ -137,6 +137,10 @@ def clean_bench(dev, steps):
         out = torch.empty(xd.shape, dtype=torch.float64, device=dev)
 
         def masks():
+            # every step from scratch: the channel-means cache (kept per tensor version so
+            # that measure_channel_variability reuses get_noisier_channels' pass) would
+            # otherwise skip the mean pass of every step after the first
+            clean.invalidate_channel_means()
             bad = clean.get_noisier_channels(xd)
             return clean.measure_channel_variability(xd, badchans_mask=bad), bad
 

@@ -44,7 +44,8 @@ means = clean.channel_means_device(x)
 plane = nchan * n * b_in
 steps = {
     # algorithmic bytes: one read of the filterbank (+ its per-row outputs)
-    "means": (lambda: clean.channel_means_device(x), plane),
+    # invalidate first: the channel-means cache would return the previous step's means
+    "means": (lambda: (clean.invalidate_channel_means(), clean.channel_means_device(x))[1], plane),
     "var": (lambda: clean.channel_variances_device(x, means), plane),
     # col means (1 read) + factor-weighted row sums (1 read + factor) + apply
     # (1 read + float64 write + column means); small 1-D passes counted too
