@@ -165,7 +165,10 @@ def clean_bench(dev, steps):
         # per-channel mean of x*f and the apply pass each read x once; the apply pass
         # writes the float64 plane (1-D vectors and the zeroed columns are negligible)
         alg = n_el * (3 * b_in + 8)
-        mask_bytes = n_el * 2 * b_in  # channel means + variances: two row passes
+        # one read pass: the means and the shifted moments come from the same pass and the
+        # std decisions are certified from them (a second, exact pass only when one is
+        # within its rounding bound: not at C4)
+        mask_bytes = n_el * b_in
         res[dt] = {"masks_ms": round(t_mask, 4), "renormalize_ms": round(t_ren, 4),
                    "renormalize_alg_bytes": alg,
                    "renormalize_GBps": round(alg / t_ren / 1e6, 1),

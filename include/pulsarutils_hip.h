@@ -202,6 +202,17 @@ int pu_row_sums(const void *x, int dtype, int64_t nrows, int64_t n, int64_t ld, 
                 void *workspace, size_t workspace_bytes, void *stream);
 size_t pu_row_sums_workspace_bytes(int64_t nrows, int64_t n);
 
+/* One pass for get_noisier_channels + measure_channel_variability (clean.py:60, 119):
+ * means[r] = ndarray.mean(1) exactly as pu_row_sums mode 0 with divisor n (f32 for f32
+ * input, else f64), and moments[3 r .. 3 r + 2] = (c, sum(x - c), sum((x - c)^2)) in
+ * float64, c = x[r, 0], summed in no particular order.  The caller certifies the
+ * std-based decisions from the moments (pulsarutils.clean._certified_variability) and
+ * runs the exact second pass (pu_row_sums mode 1) only when one is within its rounding
+ * bound.  ws: pu_row_moments_workspace_bytes(nrows, n), 8-byte aligned. */
+int pu_row_moments(const void *x, int dtype, int64_t nrows, int64_t n, int64_t ld, void *means,
+                   double *moments, void *workspace, size_t workspace_bytes, void *stream);
+size_t pu_row_moments_workspace_bytes(int64_t nrows, int64_t n);
+
 /* Column means over the rows with skip[r] == 0, sequential in row order
  * (renormalize_data's zero-DM light curve, clean.py:77).  out: device [n] f64. */
 int pu_col_means(const void *x, int dtype, int64_t nrows, int64_t n, int64_t ld,

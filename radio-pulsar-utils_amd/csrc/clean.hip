@@ -128,13 +128,18 @@ __device__ __forceinline__ Ta elem_val(Tin x, Ta center, double s)
 // the scale pairs of MODE 2) are single 2-element vector loads.  A workgroup sums
 // the same block of R consecutive rows, so MODE 2 reads its scale pairs once per R
 // rows instead of once per row.
-template <typename Tin, typename Ta, int MODE, bool PAIR, int R>
+//
+// MOM (MODE 0, pu_row_moments): the same pass also sums, in float64 and in any order,
+// d = x - c and d^2 with c = the row's first element - the shifted moments from which
+// measure_channel_variability's std is certified without a second pass (clean.py).
+template <typename Tin, typename Ta, int MODE, bool PAIR, int R, bool MOM = false>
 __global__ void __launch_bounds__(256)
 rowsum_chunk_kernel(const Tin *__restrict__ x, int64_t ld, int64_t nrows, int64_t nfull, int64_t nblk_row,
                     const Ta *__restrict__ centers, const double *__restrict__ scale,
-                    Ta *__restrict__ block_sums)
+                    Ta *__restrict__ block_sums, double *__restrict__ moments = nullptr)
 {
     __shared__ Ta wave_tot[R][4];
+    __shared__ double mom_tot[2][4];
     const int64_t row0 = (blockIdx.x / nfull) * R;
     const int64_t blk = blockIdx.x % nfull;
     const int tid = threadIdx.x;
@@ -183,18 +188,42 @@ rowsum_chunk_kernel(const Tin *__restrict__ x, int64_t ld, int64_t nrows, int64_
 #pragma unroll
         for (int s = 1; s < 64; s <<= 1) t += __shfl_xor(t, s, 64);
         if ((tid & 63) == 0) wave_tot[rr][tid >> 6] = t;
+        if constexpr (MOM) {
+            const double cs = static_cast<double>(x[row * ld]);
+            double m1 = 0.0, m2 = 0.0;
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+                const double da = static_cast<double>(a[m]) - cs, dc = static_cast<double>(c[m]) - cs;
+                m1 += da + dc;
+                m2 += da * da + dc * dc;
+            }
+#pragma unroll
+            for (int s = 1; s < 64; s <<= 1) {
+                m1 += __shfl_xor(m1, s, 64);
+                m2 += __shfl_xor(m2, s, 64);
+            }
+            if ((tid & 63) == 0) {
+                mom_tot[0][tid >> 6] = m1;
+                mom_tot[1][tid >> 6] = m2;
+            }
+        }
     }
     __syncthreads();
     if (tid < R && row0 + tid < nrows)
         block_sums[(row0 + tid) * nblk_row + blk] =
             (wave_tot[tid][0] + wave_tot[tid][1]) + (wave_tot[tid][2] + wave_tot[tid][3]);
+    if constexpr (MOM) {
+        if (tid < 2 && row0 < nrows)
+            moments[(row0 * nblk_row + blk) * 2 + tid] =
+                (mom_tot[tid][0] + mom_tot[tid][1]) + (mom_tot[tid][2] + mom_tot[tid][3]);
+    }
 }
 
-template <typename Tin, typename Ta, int MODE>
+template <typename Tin, typename Ta, int MODE, bool MOM = false>
 __global__ void __launch_bounds__(64)
 rowsum_tail_kernel(const Tin *__restrict__ x, int64_t ld, int64_t nrows, int64_t n, int64_t nfull,
                    int64_t nblk_row, const Ta *__restrict__ centers, const double *__restrict__ scale,
-                   Ta *__restrict__ block_sums)
+                   Ta *__restrict__ block_sums, double *__restrict__ moments = nullptr)
 {
     const int64_t row = (int64_t)blockIdx.x * 64 + threadIdx.x;
     if (row >= nrows) return;
@@ -202,6 +231,35 @@ rowsum_tail_kernel(const Tin *__restrict__ x, int64_t ld, int64_t nrows, int64_t
     const int64_t off = nfull * kBlock;
     block_sums[row * nblk_row + nfull] =
         pairwise_lane<Tin, Ta, MODE, 10>(x + row * ld, off, n - off, center, scale);
+    if constexpr (MOM) {
+        const double cs = static_cast<double>(x[row * ld]);
+        double m1 = 0.0, m2 = 0.0;
+        for (int64_t i = off; i < n; ++i) {
+            const double d = static_cast<double>(x[row * ld + i]) - cs;
+            m1 += d;
+            m2 += d * d;
+        }
+        moments[(row * nblk_row + nfull) * 2] = m1;
+        moments[(row * nblk_row + nfull) * 2 + 1] = m2;
+    }
+}
+
+// pu_row_moments: per row (c, sum(x - c), sum((x - c)^2)), c = the row's first element,
+// from the per-block moment pairs (float64, any order).
+template <typename Tin>
+__global__ void moments_combine(const double *__restrict__ blk, const Tin *__restrict__ x, int64_t ld,
+                                int64_t nrows, int64_t nblk_row, double *__restrict__ out)
+{
+    const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= nrows) return;
+    double m1 = 0.0, m2 = 0.0;
+    for (int64_t k = 0; k < nblk_row; ++k) {
+        m1 += blk[(row * nblk_row + k) * 2];
+        m2 += blk[(row * nblk_row + k) * 2 + 1];
+    }
+    out[row * 3] = static_cast<double>(x[row * ld]);
+    out[row * 3 + 1] = m1;
+    out[row * 3 + 2] = m2;
 }
 
 template <typename Ta>
@@ -1137,6 +1195,44 @@ int row_sums_t(const void *x, int64_t nrows, int64_t n, int64_t ld, const void *
     return pu::launch_check("rowsum_combine");
 }
 
+// numpy's row means (MODE 0 order, divided by n) and, in the same pass, the shifted
+// moments of every row (pu_row_moments).  ws: the block sums, then 2 doubles per block.
+template <typename Tin, typename Ta>
+int row_moments_t(const void *x, int64_t nrows, int64_t n, int64_t ld, void *means, double *moments, void *ws,
+                  hipStream_t s)
+{
+    const int64_t nfull = n / kBlock;
+    const int64_t tail = n % kBlock;
+    const int64_t nblk_row = nfull + (tail ? 1 : 0);
+    Ta *bs = reinterpret_cast<Ta *>(ws);
+    double *mb = reinterpret_cast<double *>(reinterpret_cast<char *>(ws) +
+                                            (((size_t)nrows * nblk_row * sizeof(double) + 255) & ~size_t(255)));
+    const Tin *xp = reinterpret_cast<const Tin *>(x);
+    if (nfull > 0) {
+        PU_REQUIRE(nrows * nfull < (int64_t(1) << 31), "pu_row_moments: too many blocks");
+        const bool pair = reinterpret_cast<uintptr_t>(x) % (2 * sizeof(Tin)) == 0 && ld % 2 == 0;
+        if (pair)
+            hipLaunchKernelGGL((rowsum_chunk_kernel<Tin, Ta, 0, true, 1, true>), dim3((unsigned)(nrows * nfull)),
+                               dim3(256), 0, s, xp, ld, nrows, nfull, nblk_row, nullptr, nullptr, bs, mb);
+        else
+            hipLaunchKernelGGL((rowsum_chunk_kernel<Tin, Ta, 0, false, 1, true>), dim3((unsigned)(nrows * nfull)),
+                               dim3(256), 0, s, xp, ld, nrows, nfull, nblk_row, nullptr, nullptr, bs, mb);
+        int rc = pu::launch_check("rowsum_chunk_kernel");
+        if (rc) return rc;
+    }
+    if (tail) {
+        hipLaunchKernelGGL((rowsum_tail_kernel<Tin, Ta, 0, true>), dim3((unsigned)((nrows + 63) / 64)), dim3(64), 0,
+                           s, xp, ld, nrows, n, nfull, nblk_row, nullptr, nullptr, bs, mb);
+        int rc = pu::launch_check("rowsum_tail_kernel");
+        if (rc) return rc;
+    }
+    hipLaunchKernelGGL((rowsum_combine<Ta>), dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, s, bs, nrows,
+                       nblk_row, (double)n, reinterpret_cast<Ta *>(means));
+    hipLaunchKernelGGL((moments_combine<Tin>), dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, s, mb, xp, ld,
+                       nrows, nblk_row, moments);
+    return pu::launch_check("moments_combine");
+}
+
 template <typename Tin>
 int row_sums_in(int mode, bool f32acc, const void *x, int64_t nrows, int64_t n, int64_t ld, const void *center,
                 const double *scale, double divisor, void *out, void *ws, hipStream_t s)
@@ -1294,6 +1390,30 @@ int pu_row_sums(const void *x, int dtype, int64_t nrows, int64_t n, int64_t ld, 
     case PU_F64: return row_sums_in<double>(mode, false, x, nrows, n, ld, center, scale, divisor, out, ws, s);
     }
     pu::set_error("pu_row_sums: unsupported dtype %d", dtype);
+    return PU_EUNSUPPORTED;
+}
+
+size_t pu_row_moments_workspace_bytes(int64_t nrows, int64_t n)
+{
+    const int64_t nblk = (n + kBlock - 1) / kBlock;
+    const size_t nb = (size_t)(nrows > 0 ? nrows : 0) * (size_t)(nblk > 0 ? nblk : 1);
+    return ((nb * sizeof(double) + 255) & ~size_t(255)) + nb * 2 * sizeof(double);
+}
+
+int pu_row_moments(const void *x, int dtype, int64_t nrows, int64_t n, int64_t ld, void *means, double *moments,
+                   void *ws, size_t ws_bytes, void *stream)
+{
+    PU_REQUIRE(x && means && moments, "pu_row_moments: NULL pointer");
+    PU_REQUIRE(nrows > 0 && n > 0 && ld >= n, "pu_row_moments: bad shape");
+    PU_REQUIRE(ws && ws_bytes >= pu_row_moments_workspace_bytes(nrows, n) && reinterpret_cast<uintptr_t>(ws) % 8 == 0,
+               "pu_row_moments: workspace too small or not 8-byte aligned");
+    hipStream_t s = pu::as_stream(stream);
+    switch (dtype) {
+    case PU_U8: return row_moments_t<uint8_t, double>(x, nrows, n, ld, means, moments, ws, s);
+    case PU_F32: return row_moments_t<float, float>(x, nrows, n, ld, means, moments, ws, s);
+    case PU_F64: return row_moments_t<double, double>(x, nrows, n, ld, means, moments, ws, s);
+    }
+    pu::set_error("pu_row_moments: unsupported dtype %d", dtype);
     return PU_EUNSUPPORTED;
 }
 

@@ -44,6 +44,8 @@ SIGNATURES = {
     "pu_plan_stamps": (_i32, [_vp, _vp, _i32]),
     "pu_row_sums": (_i32, [_vp, _i32, _i64, _i64, _i64, _i32, _vp, _vp, _f64, _vp, _vp, _sz, _vp]),
     "pu_row_sums_workspace_bytes": (_sz, [_i64, _i64]),
+    "pu_row_moments": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _sz, _vp]),
+    "pu_row_moments_workspace_bytes": (_sz, [_i64, _i64]),
     "pu_col_means": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp]),
     "pu_gaussian_filter1d": (_i32, [_vp, _i64, _vp, _i64, _vp, _vp]),
     "pu_ratio": (_i32, [_f64, _vp, _i64, _vp, _vp]),

@@ -71,27 +71,49 @@ def _row_sums(x, mode, center=None, scale=None, divisor=0.0):
     return out
 
 
-_MEANS = [None]  # (weakref to the tensor, its version counter, the means)
+_MEANS = [None]  # (weakref to the tensor, its version counter, the means, the shifted moments)
+
+
+def _row_moments(x):
+    """pu_row_moments: numpy's x.mean(1) (f32 for f32 input, else f64) and, from the same
+    read pass, per row (c, sum(x - c), sum((x - c)^2)) in float64 with c = x[r, 0]."""
+    t = _hip.torch()
+    nrows, n = x.shape
+    acc_f32 = _hip.dtype_code(x.dtype) == _hip.PU_F32
+    means = t.empty(nrows, dtype=t.float32 if acc_f32 else t.float64, device=x.device)
+    mom = t.empty((nrows, 3), dtype=t.float64, device=x.device)
+    ws = t.empty(_hip.lib().pu_row_moments_workspace_bytes(nrows, n), dtype=t.uint8, device=x.device)
+    _hip.check(_hip.lib().pu_row_moments(_hip.ptr(x), _hip.dtype_code(x.dtype), nrows, n, x.stride(0),
+                                         _hip.ptr(means), _hip.ptr(mom), _hip.ptr(ws), ws.numel(),
+                                         _hip.stream_ptr()), "pu_row_moments")
+    return means, mom
+
+
+def _cached_stats(x):
+    """(means, moments) of ``x`` from the cache, or one pu_row_moments pass (cached)."""
+    import weakref
+    c = _MEANS[0]
+    if c is not None and c[0]() is x and c[1] == (x._version, x.data_ptr()):
+        return c[2], c[3]
+    m, mom = _row_moments(x)
+    _MEANS[0] = (weakref.ref(x), (x._version, x.data_ptr()), m, mom)
+    return m, mom
 
 
 def channel_means_device(x):
     """``x.mean(1)`` with numpy's dtype and summation order (float32 stays float32).
 
-    The last result is kept for the same tensor object while it is unmodified (its
-    version counter and storage pointer unchanged): get_noisier_channels and
-    measure_channel_variability both start from the channel means of one block, and the
-    second call then skips a pass over it.  A weak reference, so the cache never keeps a
+    The pass that computes them also sums each row's shifted moments (pu_row_moments),
+    from which measure_channel_variability certifies its std decisions without a
+    second pass.  The last result is kept for the same tensor object while it is
+    unmodified (its version counter and storage pointer unchanged): get_noisier_channels
+    and measure_channel_variability both start from the statistics of one block, and the
+    second call then skips the pass.  A weak reference, so the cache never keeps a
     block alive; callers get a copy, so changing a result never changes the cache.
     Writes that bypass torch's version counter (raw-pointer kernels, DLPack aliases)
     are not seen: call :func:`invalidate_channel_means` after such a write (numpy inputs
     are copied to a fresh tensor per call and never hit the cache)."""
-    import weakref
-    c = _MEANS[0]
-    if c is not None and c[0]() is x and c[1] == (x._version, x.data_ptr()):
-        return c[2].clone()
-    m = _row_sums(x, 0, divisor=x.shape[1])
-    _MEANS[0] = (weakref.ref(x), (x._version, x.data_ptr()), m)
-    return m.clone()
+    return _cached_stats(x)[0].clone()
 
 
 def invalidate_channel_means():
@@ -149,17 +171,69 @@ def get_noisier_channels(array):
     return spec > smooth_spec + 5 * ref_mad(spec)
 
 
+def _certified_variability(means, moments, n, acc_f32, badchans_mask):
+    """measure_channel_variability's mask from one read pass, or None.
+
+    ``moments`` rows are (c, sum(x - c), sum((x - c)^2)) in float64 (pu_row_moments), so
+    V = s2 - 2 (m - c) s1 + n (m - c)^2 is the real sum of squared deviations from numpy's
+    mean m up to float64 rounding.  numpy's own std (clean.py:119, np.std in the input's
+    float type: squared deviations rounded, add.reduce of depth <= 35 + nblocks, the
+    divide and the sqrt) lies in [s_lo, s_hi] around sqrt(V / n); the quartiles of the
+    good channels (order statistics: monotone in every argument) lie in the intervals of
+    the k-th smallest bounds, and the limits 2 q1 - q2 / 2 q3 - q2 (with their three
+    roundings) in intervals built from those.  When every unmasked channel is clear of
+    both limit intervals the decisions are the reference's; otherwise (or for non-finite
+    input, or too few good channels for the reference's quartile indices) None, and the
+    caller runs the exact second pass."""
+    m = np.asarray(means, dtype=np.float64)
+    mom = np.asarray(moments, dtype=np.float64)
+    bad = np.asarray(badchans_mask, dtype=bool)
+    nchan = m.size
+    good = ~bad
+    if not (np.isfinite(m).all() and np.isfinite(mom).all()) or nchan // 4 * 3 >= int(good.sum()):
+        return None
+    c, s1, s2 = mom[:, 0], mom[:, 1], mom[:, 2]
+    dm = m - c
+    V = s2 - 2.0 * dm * s1 + n * dm * dm
+    eV = (s2 + 2.0 * np.abs(dm) * np.sqrt(n * s2) + n * dm * dm) * 2.0 ** -40 + 1e-300
+    u = 2.0 ** -24 if acc_f32 else 2.0 ** -53
+    gam = (35 + -(-n // 8192) + 4) * u
+    s_lo = np.sqrt(np.maximum(V - eV, 0.0) * (1.0 - gam) / n * (1.0 - u)) * (1.0 - u)
+    s_hi = np.sqrt((V + eV) * (1.0 + gam) / n * (1.0 + u)) * (1.0 + u)
+    lo_sorted, hi_sorted = np.sort(s_lo[good]), np.sort(s_hi[good])
+    a1, b1 = lo_sorted[nchan // 4], hi_sorted[nchan // 4]
+    a2, b2 = lo_sorted[nchan // 2], hi_sorted[nchan // 2]
+    a3, b3 = lo_sorted[nchan // 4 * 3], hi_sorted[nchan // 4 * 3]
+    r = 4.0 * u * (b2 + 2.0 * (b3 - a1)) + 1e-300  # the limits' roundings (magnitudes >= 0)
+    low_lo, low_hi = 2.0 * a1 - b2 - r, 2.0 * b1 - a2 + r
+    hi_lo, hi_hi = 2.0 * a3 - b2 - r, 2.0 * b3 - a2 + r
+    below = s_hi < low_lo
+    above = s_lo > hi_hi
+    sure = (below | (s_lo >= low_hi)) & (above | (s_hi <= hi_lo))
+    if not sure[good].all():
+        return None
+    return below | above | bad
+
+
 def measure_channel_variability(array, badchans_mask=None):
     """clean.py:114-133: per-channel std outside [q2 - 2(q2-q1), q2 + 2(q3-q2)].
 
     Quartile positions use the full channel count, as in the reference (an
     IndexError when too many channels are masked is the reference behaviour).
+    The decisions are certified from the shifted moments of the means pass
+    (_certified_variability, no second read pass); only when one is within its
+    rounding bound is numpy's std computed exactly (a second pass).
     """
     x = _hip.to_device(array)
-    spec = np.sqrt(_host(channel_variances_device(x)))
     if badchans_mask is None:
-        badchans_mask = np.zeros(spec.size, dtype=bool)
+        badchans_mask = np.zeros(x.shape[0], dtype=bool)
     badchans_mask = np.asarray(badchans_mask, dtype=bool)
+    means, mom = _cached_stats(x)
+    mask = _certified_variability(_host(means), _host(mom), x.shape[1], means.dtype == _hip.torch().float32,
+                                  badchans_mask)
+    if mask is not None:
+        return mask
+    spec = np.sqrt(_host(channel_variances_device(x, means)))
     ordered = np.sort(spec[~badchans_mask])
     q1 = ordered[spec.size // 4]
     q2 = ordered[spec.size // 2]

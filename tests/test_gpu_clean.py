@@ -137,7 +137,8 @@ def test_cut_outliers_device_certified(gpu):
     """cut_outliers runs on the device (pu_cut_outliers): the mask and the zeroed plane
     equal the reference restatement (scipy's running-sum uniform_filter1d) on random
     light curves with injected spikes and dips, N from 64 up; a NaN in a good channel
-    raises the certification flag and the host fallback gives the reference result."""
+    raises the certification flag and the exact path (on the device since round 4) gives
+    the reference result."""
     import torch
     from pulsarutils import _hip
     rng = np.random.default_rng(17)
@@ -432,3 +433,61 @@ def test_u8_row_sums_exact(gpu, n, padded):
     np.testing.assert_array_equal(C.channel_means_device(xd).cpu().numpy(), x.mean(1))
     np.testing.assert_array_equal(_chunk_row_sums(xd, 3).cpu().numpy(), x.astype(float).sum(1))
     np.testing.assert_array_equal(_chunk_row_sums(xd, 4).cpu().numpy(), (x.astype(float) ** 2).sum(1))
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.uint8, np.float64])
+@pytest.mark.parametrize("n", [8192, 20000, 262144])
+def test_row_moments_one_pass(gpu, dtype, n):
+    """pu_row_moments (round 4): the means are pu_row_sums mode 0's bit for bit (numpy's
+    mean(1)), and the shifted moments (c, sum(x - c), sum((x - c)^2)) match float64 numpy
+    to rounding - the inputs of measure_channel_variability's certification."""
+    from pulsarutils import _hip
+    rng = np.random.default_rng(n + 3)
+    x = rng.normal(100.0, 5.0, (37, n))
+    x = (np.clip(x, 0, 255) if dtype == np.uint8 else x).astype(dtype)
+    xd = _hip.to_device(x)
+    means, mom = C._row_moments(xd)
+    ref_means = C._row_sums(xd, 0, divisor=n)
+    np.testing.assert_array_equal(means.cpu().numpy(), ref_means.cpu().numpy())
+    np.testing.assert_array_equal(means.cpu().numpy(), x.mean(1))
+    xd64 = x.astype(np.float64)
+    d = xd64 - xd64[:, :1]
+    want = np.stack([xd64[:, 0], d.sum(1), (d * d).sum(1)], axis=1)
+    got = mom.cpu().numpy()
+    np.testing.assert_array_equal(got[:, 0], want[:, 0])
+    np.testing.assert_allclose(got[:, 1], want[:, 1], rtol=1e-9, atol=1e-6 * np.abs(d).sum(1).max())
+    np.testing.assert_allclose(got[:, 2], want[:, 2], rtol=1e-12)
+
+
+def test_variability_one_pass_and_fallback(gpu):
+    """measure_channel_variability: certified from the one-pass moments on ordinary data
+    (one read pass: the variance pass is not run), and the exact second pass when a
+    channel's std is moved onto the upper limit; both equal the reference."""
+    from pulsarutils import _hip
+    rng = np.random.default_rng(47)
+    nchan, n = 64, 65536
+    x = rng.normal(10.0, 1.0, (nchan, n)).astype(np.float32) * rng.uniform(0.8, 1.2, nchan)[:, None].astype(np.float32)
+    bad = np.zeros(nchan, bool)
+    bad[3] = True
+    xd = _hip.to_device(x)
+    calls = []
+    orig = C.channel_variances_device
+    C.channel_variances_device = lambda *a, **k: (calls.append(1), orig(*a, **k))[1]
+    try:
+        C.invalidate_channel_means()
+        np.testing.assert_array_equal(C.measure_channel_variability(xd, badchans_mask=bad),
+                                      co.channel_variability(x, badchans_mask=bad))
+        assert not calls  # certified: no second pass
+        # channel j (the lowest std) onto the upper limit of the others
+        spec = np.std(x, axis=1)
+        j = int(np.argmin(np.where(bad, np.inf, spec)))
+        rest = np.sort(np.delete(spec, [j, 3]))
+        q2, q3 = rest[nchan // 2], rest[nchan // 4 * 3]
+        hi = q2 + 2 * (q3 - q2)
+        x[j] = ((x[j].astype(np.float64) - x[j].mean()) * (float(hi) / float(spec[j])) + 10.0).astype(np.float32)
+        want = co.channel_variability(x, badchans_mask=bad)
+        C.invalidate_channel_means()
+        got = C.measure_channel_variability(_hip.to_device(x), badchans_mask=bad)
+        np.testing.assert_array_equal(got, want)
+    finally:
+        C.channel_variances_device = orig
