@@ -89,15 +89,30 @@ def _row_moments(x):
     return means, mom
 
 
-def _cached_stats(x):
-    """(means, moments) of ``x`` from the cache, or one pu_row_moments pass (cached)."""
+def _cached_stats(x, host=False):
+    """(means, moments) of ``x`` from the cache, or one pu_row_moments pass (cached).
+
+    The pass also starts an asynchronous copy of [means | moments] (float64, nrows x 4)
+    to pinned host memory, so that measure_channel_variability - which needs them on the
+    host - usually finds them there after get_noisier_channels' own synchronisation
+    instead of waiting for a copy of its own.  ``host=True`` returns that host array
+    (waiting for the copy) in place of the device moments."""
     import weakref
+    t = _hip.torch()
     c = _MEANS[0]
-    if c is not None and c[0]() is x and c[1] == (x._version, x.data_ptr()):
-        return c[2], c[3]
-    m, mom = _row_moments(x)
-    _MEANS[0] = (weakref.ref(x), (x._version, x.data_ptr()), m, mom)
-    return m, mom
+    if not (c is not None and c[0]() is x and c[1] == (x._version, x.data_ptr())):
+        m, mom = _row_moments(x)
+        both = t.cat([m.to(t.float64)[:, None], mom], dim=1)
+        hbuf = t.empty(both.shape, dtype=t.float64, pin_memory=True)
+        hbuf.copy_(both, non_blocking=True)
+        ev = t.cuda.Event()
+        ev.record()
+        c = (weakref.ref(x), (x._version, x.data_ptr()), m, mom, hbuf, ev)
+        _MEANS[0] = c
+    if host:
+        c[5].synchronize()
+        return c[2], c[4].numpy()
+    return c[2], c[3]
 
 
 def channel_means_device(x):
@@ -228,9 +243,9 @@ def measure_channel_variability(array, badchans_mask=None):
     if badchans_mask is None:
         badchans_mask = np.zeros(x.shape[0], dtype=bool)
     badchans_mask = np.asarray(badchans_mask, dtype=bool)
-    means, mom = _cached_stats(x)
-    mask = _certified_variability(_host(means), _host(mom), x.shape[1], means.dtype == _hip.torch().float32,
-                                  badchans_mask)
+    t = _hip.torch()
+    means, both = _cached_stats(x, host=True)  # [means (exact in float64) | moments] on the host
+    mask = _certified_variability(both[:, 0], both[:, 1:], x.shape[1], means.dtype == t.float32, badchans_mask)
     if mask is not None:
         return mask
     spec = np.sqrt(_host(channel_variances_device(x, means)))
