@@ -730,20 +730,30 @@ __global__ void __launch_bounds__(1024) outlier_std_kernel(const double *__restr
     }
 }
 
-// Certified decisions, one lane per time bin: the mask and the flag (an ambiguous
-// comparison raises it; outlier_exact_kernel then redoes the mask).
+// Certified decisions, one lane per time bin: the mask, the flag (an ambiguous
+// comparison raises it; outlier_exact_kernel then redoes the mask) and the list of the
+// bad bins (st->nbad entries; one atomic per wave that has any, lanes in column order).
 __global__ void __launch_bounds__(256)
-outlier_mask_kernel(const double *__restrict__ u, int64_t n, OutlierState *st, uint8_t *__restrict__ mask)
+outlier_mask_kernel(const double *__restrict__ u, int64_t n, OutlierState *st, uint8_t *__restrict__ mask,
+                    int32_t *__restrict__ list)
 {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const double v = u[i];
-    const double du = v - st->up, dd = v - st->down;
-    const bool amb = !(fabs(du) > st->margin_up) || !(fabs(dd) > st->margin_down);
-    if (amb) atomicOr(&st->flag, 1u);
-    const uint8_t b = (du > 0.0 || dd < 0.0) ? 1 : 0;
-    mask[i] = b;
-    if (b) atomicAdd(&st->nbad, 1u);
+    uint8_t b = 0;
+    if (i < n) {
+        const double v = u[i];
+        const double du = v - st->up, dd = v - st->down;
+        const bool amb = !(fabs(du) > st->margin_up) || !(fabs(dd) > st->margin_down);
+        if (amb) atomicOr(&st->flag, 1u);
+        b = (du > 0.0 || dd < 0.0) ? 1 : 0;
+        mask[i] = b;
+    }
+    const uint64_t bal = __ballot(b != 0);
+    if (!bal) return;
+    const int lane = threadIdx.x & 63;
+    uint32_t base = 0;
+    if (lane == __ffsll((unsigned long long)bal) - 1) base = atomicAdd(&st->nbad, (uint32_t)__popcll(bal));
+    base = __shfl(base, __ffsll((unsigned long long)bal) - 1, 64);
+    if (b) list[base + __popcll(bal & ((uint64_t(1) << lane) - 1))] = (int32_t)i;
 }
 
 // numpy add.reduce of a contiguous double vector (0 + pairwise sums of 8192-element
@@ -776,7 +786,7 @@ __device__ double reduce_sum_staged(const double *__restrict__ a, int64_t m, dou
 // (tests/test_oracle.py::test_cut_outliers_exact_restatement).
 __global__ void __launch_bounds__(256)
 outlier_exact_kernel(const double *__restrict__ lc, int64_t n, OutlierState *st, double *__restrict__ v,
-                     double *__restrict__ tmp, uint8_t *__restrict__ mask, int force)
+                     double *__restrict__ tmp, uint8_t *__restrict__ mask, int32_t *__restrict__ list, int force)
 {
     if (!force && st->flag == 0) return;
     __shared__ double stage[kBlock];
@@ -829,37 +839,25 @@ outlier_exact_kernel(const double *__restrict__ lc, int64_t n, OutlierState *st,
     }
     __syncthreads();
     __threadfence_block();
-    unsigned cnt = 0;
     for (int64_t i = t; i < n; i += 256) {
         const double x = v[i];
         const uint8_t b = (x > thr[0] || x < thr[1]) ? 1 : 0;
         mask[i] = b;
-        cnt += b;
+        if (b) list[atomicAdd(&st->nbad, 1u)] = (int32_t)i;  // any order: the zeroing is idempotent
     }
-    if (cnt) atomicAdd(&st->nbad, cnt);
 }
 
-// Per 64 columns: zero the plane's bad columns (the final mask), rows strided over the
-// block's 4 waves.
+// Zero the plane's bad columns (the final list): one workgroup per row, the list's
+// entries over the lanes (entries of a wave are consecutive columns of a burst, so the
+// stores coalesce).  Row-major: each row's 2 MiB page is touched by one workgroup instead
+// of once per 64-column block of bad bins (15 us -> a few at C4).
 __global__ void __launch_bounds__(256)
-outlier_zero_kernel(const uint8_t *__restrict__ mask, int64_t n, double *__restrict__ out, int64_t nrows, int64_t ld)
+outlier_zero_kernel(const int32_t *__restrict__ list, const OutlierState *st, double *__restrict__ out,
+                    int64_t nrows, int64_t ld)
 {
-    __shared__ uint8_t bad[64];
-    __shared__ int any;
-    const int64_t c0 = (int64_t)blockIdx.x * 64;
-    const int t = threadIdx.x;
-    if (t == 0) any = 0;
-    __syncthreads();
-    if (t < 64) {
-        const uint8_t b = c0 + t < n ? mask[c0 + t] : 0;
-        bad[t] = b;
-        if (b) any = 1;
-    }
-    __syncthreads();
-    if (!any) return;
-    const int col = t & 63;
-    if (!bad[col]) return;
-    for (int64_t r = t >> 6; r < nrows; r += 4) out[r * ld + c0 + col] = 0.0;
+    const uint32_t nbad = st->nbad;
+    double *row = out + (int64_t)blockIdx.x * ld;
+    for (uint32_t k = threadIdx.x; k < nbad; k += 256) row[list[k]] = 0.0;
 }
 
 __global__ void zero_cols_kernel(double *out, int64_t nrows, int64_t ld, const int64_t *__restrict__ cols,
@@ -1495,7 +1493,7 @@ int pu_renorm_apply_zero_dm(const void *x, int dtype, int64_t nchan, int64_t n, 
 size_t pu_cut_outliers_workspace_bytes(int64_t n)
 {
     const size_t m = (size_t)(n > 0 ? n : 0);
-    return 256 + (m + (m + 15) / 16) * sizeof(double);  // state | window means | every 16th
+    return 256 + (m + (m + 15) / 16) * sizeof(double) + m * sizeof(int32_t);  // state | window means | every 16th | bad list
 }
 
 namespace {
@@ -1509,15 +1507,18 @@ int cut_outliers(const double *lc, int64_t n, double *out, int64_t nrows, int64_
     OutlierState *st = reinterpret_cast<OutlierState *>(ws);
     double *u = reinterpret_cast<double *>(reinterpret_cast<char *>(ws) + 256);
     double *u16 = u + n;
+    int32_t *list = reinterpret_cast<int32_t *>(u16 + (n + 15) / 16);
+    PU_REQUIRE(nrows < (int64_t(1) << 31), "pu_cut_outliers: too many rows");
     PU_TRY_HIP(hipMemsetAsync(st, 0, sizeof(OutlierState), s));
     if (!exact_only) {
         hipLaunchKernelGGL(outlier_window_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, lc, n, u, u16, st);
         hipLaunchKernelGGL(outlier_std_kernel, dim3(1), dim3(1024), 0, s, u16, n, st);
-        hipLaunchKernelGGL(outlier_mask_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, u, n, st, mask);
+        hipLaunchKernelGGL(outlier_mask_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, u, n, st, mask, list);
     }
     // returns at once unless the flag is set (or exact_only)
-    hipLaunchKernelGGL(outlier_exact_kernel, dim3(1), dim3(256), 0, s, lc, n, st, u, u16, mask, exact_only ? 1 : 0);
-    hipLaunchKernelGGL(outlier_zero_kernel, dim3(blocks_for(n, 64)), dim3(256), 0, s, mask, n, out, nrows, ld_out);
+    hipLaunchKernelGGL(outlier_exact_kernel, dim3(1), dim3(256), 0, s, lc, n, st, u, u16, mask, list,
+                       exact_only ? 1 : 0);
+    hipLaunchKernelGGL(outlier_zero_kernel, dim3((unsigned)nrows), dim3(256), 0, s, list, st, out, nrows, ld_out);
     return pu::launch_check("outlier kernels");
 }
 }  // namespace
