@@ -520,6 +520,92 @@ gauss_pair_kernel(const double *__restrict__ x, int64_t n, const double *__restr
     if (i + 1 < n) out[i + 1] = a1;
 }
 
+// Quad form (round 4, the default for r <= kGaussMaxR): each thread computes FOUR adjacent
+// outputs i..i+3 from two sliding register windows, left x[i+j .. i+j+3] and right
+// x[i-j .. i-j+3]; per two taps one new 16-B pair enters each window, so the LDS traffic
+// per output-tap is 4 B (pair form: 12 B) plus a broadcast weight pair.  The next two
+// taps' pairs are read one iteration ahead.  1024 outputs per workgroup (one workgroup per CU
+// at n = 2^18, one wave per SIMD: the f64 adds, not LDS, set the pace).  Per output the
+// order is scipy's: acc = x[i] w[r], then acc += (x[i+j] + x[i-j]) w[r+j], j = -r..-1.
+constexpr int kGaussQuadOut = 1024;
+
+__global__ void __launch_bounds__(256)
+gauss_quad_kernel(const double *__restrict__ x, int64_t n, const double *__restrict__ w, int r,
+                  double *__restrict__ out)
+{
+    extern __shared__ __attribute__((aligned(16))) double gsm4[];
+    const int wn = (r + 2) & ~1;  // weights padded to an even count: the window stays 16-B aligned
+    double *ws = gsm4;
+    double *xs = gsm4 + wn;       // x[i0 - r - pad, i0 + 1024 + r + pad), reflected at staging
+    const int64_t i0 = (int64_t)blockIdx.x * kGaussQuadOut;
+    const int span = kGaussQuadOut + 2 * r + 2 * kGaussPad;
+    for (int k = threadIdx.x; k < wn; k += 256) ws[k] = k <= r ? w[k] : 0.0;
+    for (int k = threadIdx.x; k < span; k += 256) {
+        const int64_t g = i0 - r - kGaussPad + k;
+        xs[k] = x[(g >= 0 && g < n) ? g : reflect_index(g, n)];
+    }
+    __syncthreads();
+    const int t4 = 4 * (int)threadIdx.x;
+    const int64_t i = i0 + t4;
+    // xc[q] = x[i + q]; xc + m is 16-B aligned whenever m + r is even (pad even, t4 even)
+    const double *xc = xs + t4 + r + kGaussPad;
+    auto pair = [&](int m) { return *reinterpret_cast<const f64x2 *>(xc + m); };
+    auto wpair = [&](int m) { return *reinterpret_cast<const f64x2 *>(ws + r + m); };  // w[r+m], w[r+m+1]
+    const double wr = ws[r];
+    double a[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[q] = xc[q] * wr;
+    int j = -r;
+    f64x2 l01 = pair(j), l23 = pair(j + 2);    // left  window xc[j .. j+3]
+    f64x2 r01 = pair(-j), r23 = pair(-j + 2);  // right window xc[-j .. -j+3]
+    // the next two taps' window and weight pairs are read one iteration ahead (one wave per
+    // SIMD: nothing else covers the LDS latency)
+    f64x2 p = {0.0, 0.0}, s = {0.0, 0.0}, wp = {0.0, 0.0};
+    if (r >= 2) {
+        p = pair(j + 4);   // xc[j+4], xc[j+5]
+        s = pair(-j - 2);  // xc[-j-2], xc[-j-1]
+        wp = wpair(j);
+    }
+#pragma unroll 2
+    for (; j + 1 < 0; j += 2) {
+        const int jn = j + 3 < 0 ? j + 2 : j;  // the last iteration reloads its own (in bounds)
+        const f64x2 pn = pair(jn + 4), sn = pair(-jn - 2), wpn = wpair(jn);
+        const double w0 = wp.x, w1 = wp.y;
+        // tap j: left xc[j+q], right xc[q-j]
+        a[0] += (l01.x + r01.x) * w0;
+        a[1] += (l01.y + r01.y) * w0;
+        a[2] += (l23.x + r23.x) * w0;
+        a[3] += (l23.y + r23.y) * w0;
+        // tap j+1: left xc[j+1+q], right xc[q-j-1]
+        a[0] += (l01.y + s.y) * w1;
+        a[1] += (l23.x + r01.x) * w1;
+        a[2] += (l23.y + r01.y) * w1;
+        a[3] += (p.x + r23.x) * w1;
+        l01 = l23;
+        l23 = p;
+        r23 = r01;
+        r01 = s;
+        p = pn;
+        s = sn;
+        wp = wpn;
+    }
+    if (j < 0) {  // odd r: the last tap, j = -1
+        const double w0 = ws[r - 1];
+        a[0] += (l01.x + r01.x) * w0;
+        a[1] += (l01.y + r01.y) * w0;
+        a[2] += (l23.x + r23.x) * w0;
+        a[3] += (l23.y + r23.y) * w0;
+    }
+    if (i + 3 < n && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+        *reinterpret_cast<f64x2 *>(out + i) = f64x2{a[0], a[1]};
+        *reinterpret_cast<f64x2 *>(out + i + 2) = f64x2{a[2], a[3]};
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (i + q < n) out[i + q] = a[q];
+    }
+}
+
 __global__ void ratio_kernel(double num, const double *__restrict__ x, int64_t n, double *__restrict__ out)
 {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1441,10 +1527,17 @@ int pu_gaussian_filter1d(const double *x, int64_t n, const double *w, int64_t r,
                                n, w, (int)r, out);
             return pu::launch_check("gauss_lds_kernel");
         }
-        const size_t lds = (size_t)(((r + 2) & ~int64_t(1)) + 512 + 2 * r + 2 * kGaussPad) * sizeof(double);
-        hipLaunchKernelGGL(gauss_pair_kernel, dim3(blocks_for(n, 512)), dim3(256), lds, pu::as_stream(stream), x, n,
-                           w, (int)r, out);
-        return pu::launch_check("gauss_pair_kernel");
+        static const bool pair = pu::knob("PU_GAUSS_PAIR", 0) != 0;  // the round-3 two-output form, for A/B
+        if (pair) {
+            const size_t lds = (size_t)(((r + 2) & ~int64_t(1)) + 512 + 2 * r + 2 * kGaussPad) * sizeof(double);
+            hipLaunchKernelGGL(gauss_pair_kernel, dim3(blocks_for(n, 512)), dim3(256), lds, pu::as_stream(stream), x,
+                               n, w, (int)r, out);
+            return pu::launch_check("gauss_pair_kernel");
+        }
+        const size_t lds = (size_t)(((r + 2) & ~int64_t(1)) + kGaussQuadOut + 2 * r + 2 * kGaussPad) * sizeof(double);
+        hipLaunchKernelGGL(gauss_quad_kernel, dim3(blocks_for(n, kGaussQuadOut)), dim3(256), lds,
+                           pu::as_stream(stream), x, n, w, (int)r, out);
+        return pu::launch_check("gauss_quad_kernel");
     }
     hipLaunchKernelGGL(gauss_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, pu::as_stream(stream), x, n, w, r, out);
     return pu::launch_check("gauss_kernel");
@@ -1509,7 +1602,9 @@ int cut_outliers(const double *lc, int64_t n, double *out, int64_t nrows, int64_
     double *u16 = u + n;
     int32_t *list = reinterpret_cast<int32_t *>(u16 + (n + 15) / 16);
     PU_REQUIRE(nrows < (int64_t(1) << 31), "pu_cut_outliers: too many rows");
-    PU_TRY_HIP(hipMemsetAsync(st, 0, sizeof(OutlierState), s));
+    // one 16-byte-multiple fill (the runtime splits a 56-byte memset into two kernels)
+    static_assert(sizeof(OutlierState) <= 64, "OutlierState fits the cleared 64 bytes");
+    PU_TRY_HIP(hipMemsetAsync(st, 0, 64, s));
     if (!exact_only) {
         hipLaunchKernelGGL(outlier_window_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, lc, n, u, u16, st);
         hipLaunchKernelGGL(outlier_std_kernel, dim3(1), dim3(1024), 0, s, u16, n, st);

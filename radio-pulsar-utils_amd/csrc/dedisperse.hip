@@ -2520,12 +2520,13 @@ CertModel cert_model(const pu_plan *p)
     return m;
 }
 
+// cleared: the caller already zeroed the certification state earlier in the stream
 int launch_finalize(pu_plan *p, const void *part, double *mx, double *sd, double *snr, int32_t *win, char *ws,
-                    hipStream_t s)
+                    hipStream_t s, bool cleared = false)
 {
     CertState *cert = reinterpret_cast<CertState *>(ws + part_bytes(p));
     int32_t *list = reinterpret_cast<int32_t *>(cert + 1);
-    PU_TRY_HIP(hipMemsetAsync(cert, 0, sizeof(CertState), s));
+    if (!cleared) PU_TRY_HIP(hipMemsetAsync(cert, 0, sizeof(CertState), s));
     if (part_elem(p) == sizeof(float))
         hipLaunchKernelGGL(pu_finalize_kernel<float>, dim3((unsigned)p->ndm), dim3(256), 0, s,
                            reinterpret_cast<const float *>(part), p->ntt, (int)p->n, p->TT, mx, sd, snr, win, cert_model(p),
@@ -2938,10 +2939,14 @@ int pu_plan_search(pu_plan *p, const void *data, int64_t ld, double *max_out, do
     DedispArgs a = make_args(p, data, ld);
     a.partials = workspace;
     hipStream_t s = pu::as_stream(stream);
+    char *ws = reinterpret_cast<char *>(workspace);
+    // the certification state is cleared BEFORE the search kernel: the fill then runs while
+    // the stream is idle after the previous call's host read, instead of between the search
+    // and finalize kernels (C5: ~10 us of fill + dispatch gap on the step)
+    PU_TRY_HIP(hipMemsetAsync(ws + part_bytes(p), 0, sizeof(CertState), s));
     rc = dispatch(p, a, false, s);
     if (rc) return rc;
-    char *ws = reinterpret_cast<char *>(workspace);
-    rc = launch_finalize(p, a.partials, max_out, std_out, snr_out, rebin_out, ws, s);
+    rc = launch_finalize(p, a.partials, max_out, std_out, snr_out, rebin_out, ws, s, true);
     if (rc) return rc;
     return resolve_flagged(p, data, ld, max_out, std_out, snr_out, rebin_out, ws, s);
 }
