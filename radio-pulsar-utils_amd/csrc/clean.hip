@@ -527,9 +527,10 @@ gauss_pair_kernel(const double *__restrict__ x, int64_t n, const double *__restr
 // taps' pairs are read one iteration ahead.  1024 outputs per workgroup (one workgroup per CU
 // at n = 2^18, one wave per SIMD: the f64 adds, not LDS, set the pace).  Per output the
 // order is scipy's: acc = x[i] w[r], then acc += (x[i+j] + x[i-j]) w[r+j], j = -r..-1.
-constexpr int kGaussQuadOut = 1024;
+constexpr int kGaussQuadThreads = 256;
 
-__global__ void __launch_bounds__(256)
+template <int T>
+__global__ void __launch_bounds__(T)
 gauss_quad_kernel(const double *__restrict__ x, int64_t n, const double *__restrict__ w, int r,
                   double *__restrict__ out)
 {
@@ -537,12 +538,17 @@ gauss_quad_kernel(const double *__restrict__ x, int64_t n, const double *__restr
     const int wn = (r + 2) & ~1;  // weights padded to an even count: the window stays 16-B aligned
     double *ws = gsm4;
     double *xs = gsm4 + wn;       // x[i0 - r - pad, i0 + 1024 + r + pad), reflected at staging
-    const int64_t i0 = (int64_t)blockIdx.x * kGaussQuadOut;
-    const int span = kGaussQuadOut + 2 * r + 2 * kGaussPad;
-    for (int k = threadIdx.x; k < wn; k += 256) ws[k] = k <= r ? w[k] : 0.0;
-    for (int k = threadIdx.x; k < span; k += 256) {
-        const int64_t g = i0 - r - kGaussPad + k;
-        xs[k] = x[(g >= 0 && g < n) ? g : reflect_index(g, n)];
+    const int64_t i0 = (int64_t)blockIdx.x * (4 * T);
+    const int span = (4 * T) + 2 * r + 2 * kGaussPad;
+    for (int k = threadIdx.x; k < wn; k += T) ws[k] = k <= r ? w[k] : 0.0;
+    const int64_t g0 = i0 - r - kGaussPad;
+    if (g0 >= 0 && g0 + span <= n) {  // interior workgroup (uniform): no reflection
+        for (int k = threadIdx.x; k < span; k += T) xs[k] = x[g0 + k];
+    } else {
+        for (int k = threadIdx.x; k < span; k += T) {
+            const int64_t g = g0 + k;
+            xs[k] = x[(g >= 0 && g < n) ? g : reflect_index(g, n)];
+        }
     }
     __syncthreads();
     const int t4 = 4 * (int)threadIdx.x;
@@ -1534,9 +1540,17 @@ int pu_gaussian_filter1d(const double *x, int64_t n, const double *w, int64_t r,
                                n, w, (int)r, out);
             return pu::launch_check("gauss_pair_kernel");
         }
-        const size_t lds = (size_t)(((r + 2) & ~int64_t(1)) + kGaussQuadOut + 2 * r + 2 * kGaussPad) * sizeof(double);
-        hipLaunchKernelGGL(gauss_quad_kernel, dim3(blocks_for(n, kGaussQuadOut)), dim3(256), lds,
-                           pu::as_stream(stream), x, n, w, (int)r, out);
+        // threads per workgroup (4 outputs each): PU_GAUSS_THREADS 64 / 128 / 256 (A/B)
+        const int gt = pu::knob("PU_GAUSS_THREADS", kGaussQuadThreads);
+        auto quad = [&](auto tc) {
+            constexpr int T = decltype(tc)::value;
+            const size_t lds = (size_t)(((r + 2) & ~int64_t(1)) + 4 * T + 2 * r + 2 * kGaussPad) * sizeof(double);
+            hipLaunchKernelGGL(gauss_quad_kernel<T>, dim3(blocks_for(n, 4 * T)), dim3(T), lds, pu::as_stream(stream),
+                               x, n, w, (int)r, out);
+        };
+        if (gt <= 64) quad(std::integral_constant<int, 64>{});
+        else if (gt <= 128) quad(std::integral_constant<int, 128>{});
+        else quad(std::integral_constant<int, 256>{});
         return pu::launch_check("gauss_quad_kernel");
     }
     hipLaunchKernelGGL(gauss_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, pu::as_stream(stream), x, n, w, r, out);
