@@ -137,3 +137,32 @@ def test_series_stats_bitexact_vs_oracle(gpu):
             want = oracle.trial_stats(r)
             np.testing.assert_array_equal(np.array([g[i] for g in got[:3]]), np.array(want[:3]), err_msg=f"n={n} row {i}")
             assert got[3][i] == want[3], (n, i, got[3][i], want[3])
+
+
+def test_nearconst_f32_c2_shape_vs_oracle(gpu):
+    """A near-constant float32 filterbank at C2's shape (1024 x 2^20: 1000 + 1e-3 N(0, 1)),
+    through the default float32-accumulation subband search (pinned
+    only at 32 x 4096 before).  The float32 series sums (~1e6, ulp 0.06) round by more than
+    the series' std (~0.03), so the certification must refuse every trial's
+    fast statistics and recompute them exactly: all four columns then equal the C oracle's
+    float64 channel-order restatement of the reference (dedispersion.py:86-98, 186-201) bit
+    for bit.  Parity against the oracle, not a reference-run golden (the oracle is pinned to
+    the reference's own tables elsewhere, tests/test_oracle.py)."""
+    import torch
+    nchan, n = DC.SHAPES["c2"][:2]
+    _, f0, bw, ts = DC.band("c2:zero:f32")
+    dms = DC.trial_dms("c2")
+    rng = np.random.default_rng(20261018)
+    x = rng.standard_normal((nchan, n), dtype=np.float32)
+    x *= np.float32(1e-3)
+    x += np.float32(1000.0)
+    xd = torch.from_numpy(x).cuda()
+    (mx, sd, snr, win), plan = D.search_device(xd, dms, nchan, f0, bw, ts)
+    got = [v.cpu().numpy() for v in (mx, sd, snr, win)]
+    del xd
+    assert plan.info["group"] > 1, plan.info   # the subband (fast) kernel ran
+    info = plan.cert_info()
+    assert info["rechecked"] == dms.size, info
+    ref = oracle.search(x, dms, f0, bw, ts, nthreads=16)
+    for col, (g, r) in enumerate(zip(got, ref)):
+        np.testing.assert_array_equal(g, r, err_msg=f"nearconst c2 col {col}")
