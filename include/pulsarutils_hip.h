@@ -147,6 +147,16 @@ int pu_series_stats(const double *series, int64_t rows, int64_t n, int64_t ld,
 int pu_plan_dedisperse(pu_plan *plan, const void *data, int64_t ld, void *plane,
                        int64_t ld_plane, void *stream);
 
+/* The plan's DM tiles in launch order (tile t = trials first[t] .. first[t] + count[t] - 1);
+ * writes up to ``n`` of each (either pointer may be NULL) and returns the tile count. */
+int pu_plan_dm_tiles(const pu_plan *plan, int32_t *first, int32_t *count, int n);
+/* pu_plan_dedisperse restricted to one DM tile ``dt`` of the plan: the tile's trials'
+ * rows (dedispersion.py:93-98) at plane rows 0 .. count[dt] - 1, computed by the very
+ * kernel instantiation, tables and tiling a full launch of the plan uses (parity tests
+ * of a production plan's series at full size without its whole plane). */
+int pu_plan_dedisperse_dm_tile(pu_plan *plan, const void *data, int64_t ld, int64_t dt,
+                               void *plane, int64_t ld_plane, void *stream);
+
 /* Measurement (bench.py): record a HIP event pair on the launch stream around each
  * of the next ``nslots`` dedispersion-kernel launches of this plan (0 disables). */
 int pu_plan_enable_timing(pu_plan *plan, int nslots);

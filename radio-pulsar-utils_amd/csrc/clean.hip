@@ -138,6 +138,8 @@ rowsum_chunk_kernel(const Tin *__restrict__ x, int64_t ld, int64_t nrows, int64_
                     const Ta *__restrict__ centers, const double *__restrict__ scale,
                     Ta *__restrict__ block_sums, double *__restrict__ moments = nullptr)
 {
+    // mom_tot has one slot per wave, not per row, and only row0's moments are stored
+    static_assert(!MOM || R == 1, "rowsum_chunk_kernel: MOM needs R == 1");
     __shared__ Ta wave_tot[R][4];
     __shared__ double mom_tot[2][4];
     const int64_t row0 = (blockIdx.x / nfull) * R;
@@ -727,8 +729,9 @@ apply_kernel(const Tin *__restrict__ x, int64_t nchan, int64_t col0, int64_t nco
 // (per-step rounding of the chain <= 1.5 2^-53 L, of the 16-term sum <= 16 2^-53 L),
 // and |std(u) - std(v)| <= max |u - v| plus rounding.  A comparison is decided only
 // when u is farther than that bound from the threshold; otherwise (or on NaN) the
-// state's flag is raised and the host redoes the step with scipy itself.  So the mask
-// equals the reference's bit for bit whenever the flag is clear.
+// state's flag is raised and outlier_exact_kernel, on the same stream, recomputes the
+// mask with scipy's running sum and numpy's std order (ws[0:4] then only reports that
+// the exact path ran).  So the mask equals the reference's bit for bit either way.
 struct OutlierState {
     uint32_t flag;             // 1: a decision was ambiguous or a value NaN (ABI: bytes 0-3)
     uint32_t nbad;             // bad time bins (ABI: bytes 4-7)

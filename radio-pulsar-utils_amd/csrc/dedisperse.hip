@@ -65,7 +65,7 @@ struct DedispArgs {
     int32_t small_n;
     int32_t tt0;      // first time tile of this launch (time-tile range launches)
     int32_t ntt_run;  // time tiles this launch covers (grid = ndt x ntt_run)
-    int32_t pad1;
+    int32_t dt0;      // first DM tile of this launch (DM-tile range launches; ndt = their count)
     void *plane;
     int64_t ld_plane;
     void *partials;  // float records for float32 accumulation, double for float64
@@ -788,7 +788,7 @@ dedisp_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const int32_
     constexpr int D = kD;
 
     const int wg = pu::xcd_remap(blockIdx.x, gridDim.x);
-    const int dt = wg % a.ndt;
+    const int dt = a.dt0 + wg % a.ndt;
     const int tt = a.tt0 + wg / a.ndt;
     const int t0 = tt * TT;
     const int tid = threadIdx.x;
@@ -1182,7 +1182,7 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
     // DM-tile-major order dispatches the longest items first (LPT: the short ones fill
     // the tail), for grids of few items per CU; time-tile-major order keeps the DM tiles
     // of one time tile together (one XCD, its L2 serving their overlapping rows).
-    const int dt = a.dt_major ? wg / o.ntt_run : wg % ndt;
+    const int dt = o.dt0 + (a.dt_major ? wg / o.ntt_run : wg % ndt);
     const int tt = o.tt0 + (a.dt_major ? wg % o.ntt_run : wg / ndt);
     const int t0 = tt * TT;
     const int tid = threadIdx.x;
@@ -1737,6 +1737,7 @@ struct pu_plan {
     int base_bits = 31;  // subband DMA row words: base bits (24: per-channel cover above them)
     size_t slot_bytes = 0, zero_len = 0;
     int64_t exec_adds = 0, lds_traffic = 0;  // per launch (measurement: bench.py roofline)
+    std::vector<int32_t> tile_first, tile_count;  // DM tiles in launch order (pu_plan_dm_tiles)
     int64_t nstages = 0;
     int dt_major = 0;  // subband item order (SubArgs::dt_major)
     int opt_u8_dma = -1, opt_dt_major = -1;  // pu_plan_opts (planner inputs)
@@ -1770,7 +1771,7 @@ int ensure_lds(Kern kern, size_t bytes)
 template <typename Tin, typename Tl, typename Ta>
 int launch_variant(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
 {
-    const dim3 grid((unsigned)((int64_t)p->ndt * a.ntt_run)), block(kThreads);
+    const dim3 grid((unsigned)((int64_t)a.ndt * a.ntt_run)), block(kThreads);
     if (plane) {
         auto kern = dedisp_kernel<Tin, Tl, Ta, true, false>;
         int rc = ensure_lds(kern, p->lds_bytes);
@@ -1818,7 +1819,7 @@ int launch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
     if (const char *env = getenv("PU_DMA_WAVES")) sa.dma_waves = std::clamp(atoi(env), 1, (int)C::W);
 #endif
 
-    const int64_t nitems = (int64_t)p->ndt * a.ntt_run;
+    const int64_t nitems = (int64_t)a.ndt * a.ntt_run;
     sa.nitems = (int32_t)nitems;
     sa.base_bits = p->base_bits;
     sa.dt_major = p->dt_major;
@@ -2049,10 +2050,11 @@ int plan_channels(pu_plan *p, const int64_t *shifts, size_t budget)
     }
     p->exec_adds = ndm * nchan * (int64_t)p->ntt * p->TT;
     // LDS bytes per launch (bench.py roofline): per time tile, the staged rows (E copies of
-    // row_stride elements per channel) and, per active wave and channel, one 4 x 8-byte
+    // row_stride elements per channel) and, per active wave and channel, one J x 8-byte
     // x 64-lane window read for the first trial and for every trial whose window differs
-    // from the previous trial's (the reload flag)
+    // from the previous trial's (the reload flag); J = p->K / E reads per window
     {
+        const int J = p->K / E;
         int64_t lds_tile = 0;
         for (size_t t = 0; t < (size_t)ndt; ++t) {
             lds_tile += nchan * (int64_t)E * p->row_stride * esz;
@@ -2061,11 +2063,13 @@ int plan_channels(pu_plan *p, const int64_t *shifts, size_t budget)
                     const u32x4 r = rec[(t * nchan + c) * kWaves + w];
                     int reads = 1;
                     for (int d = 1; d < kD; ++d) reads += (r[d >> 1] >> (16 * (d & 1))) & 0x8000u ? 1 : 0;
-                    lds_tile += reads * 4 * 64 * 8;
+                    lds_tile += (int64_t)reads * J * 64 * 8;
                 }
         }
         p->lds_traffic = lds_tile * p->ntt;
     }
+    p->tile_first = first;
+    p->tile_count = count;
     int rc = PU_OK;
     if (!rc) rc = upload(&p->d_first, first);
     if (!rc) rc = upload(&p->d_count, count);
@@ -2428,6 +2432,12 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     p->lds_traffic = lds_tile * ntt;
     // host tables only: the caller uploads the plan it keeps (upload_sub), so comparing
     // candidate group sizes costs no device memory
+    p->tile_first.resize((size_t)ndt);
+    p->tile_count.resize((size_t)ndt);
+    for (int t = 0; t < ndt; ++t) {
+        p->tile_first[t] = tiles[t].x;
+        p->tile_count[t] = tiles[t].y;
+    }
     SubHost &h = p->host;
     h.tiles = std::move(tiles);
     h.tile_stages = std::move(tile_stages);
@@ -2960,6 +2970,40 @@ int pu_plan_dedisperse(pu_plan *p, const void *data, int64_t ld, void *plane, in
     PU_REQUIRE(ld_plane >= p->n, "pu_plan_dedisperse: ld_plane < nsamples");
     DedispArgs a = make_args(p, data, ld);
     a.plane = plane;
+    a.ld_plane = ld_plane;
+    return dispatch(p, a, true, pu::as_stream(stream));
+}
+
+int pu_plan_dm_tiles(const pu_plan *p, int32_t *first, int32_t *count, int n)
+{
+    if (!p) return 0;
+    std::lock_guard<std::mutex> guard(p->lock.m);
+    const int ndt = (int)p->tile_first.size();
+    for (int t = 0; t < std::min(n, ndt); ++t) {
+        if (first) first[t] = p->tile_first[t];
+        if (count) count[t] = p->tile_count[t];
+    }
+    return ndt;
+}
+
+int pu_plan_dedisperse_dm_tile(pu_plan *p, const void *data, int64_t ld, int64_t dt, void *plane, int64_t ld_plane,
+                               void *stream)
+{
+    int rc = check_data(p, data, ld);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> guard(p->lock.m);
+    PU_REQUIRE(plane != nullptr, "pu_plan_dedisperse_dm_tile: plane is NULL");
+    PU_REQUIRE(ld_plane >= p->n, "pu_plan_dedisperse_dm_tile: ld_plane < nsamples");
+    PU_REQUIRE(0 <= dt && dt < (int64_t)p->tile_first.size(), "pu_plan_dedisperse_dm_tile: DM tile %lld outside [0, %d)",
+               (long long)dt, (int)p->tile_first.size());
+    DedispArgs a = make_args(p, data, ld);
+    a.dt0 = (int32_t)dt;
+    a.ndt = 1;
+    // the kernels write trial row (first + i) at plane + (first + i) ld_plane: shift the base
+    // so that the tile's rows land at rows 0 .. count - 1 of the caller's plane
+    const size_t elem = kVariants[p->variant].acc_f64 ? sizeof(double) : sizeof(float);
+    a.plane = reinterpret_cast<void *>(reinterpret_cast<uintptr_t>(plane) -
+                                       (uintptr_t)((size_t)p->tile_first[(size_t)dt] * (size_t)ld_plane * elem));
     a.ld_plane = ld_plane;
     return dispatch(p, a, true, pu::as_stream(stream));
 }

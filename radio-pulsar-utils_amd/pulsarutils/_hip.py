@@ -34,6 +34,8 @@ SIGNATURES = {
     "pu_plan_workspace_bytes": (_sz, [_vp]),
     "pu_plan_search": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "pu_plan_dedisperse": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp]),
+    "pu_plan_dm_tiles": (_i32, [_vp, _vp, _vp, _i32]),
+    "pu_plan_dedisperse_dm_tile": (_i32, [_vp, _vp, _i64, _i64, _vp, _i64, _vp]),
     "pu_plan_search_tiles": (_i32, [_vp, _vp, _i64, _i64, _i64, _vp, _sz, _vp]),
     "pu_plan_finalize": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "pu_series_stats_workspace_bytes": (_sz, [_i64, _i64]),
@@ -392,6 +394,29 @@ class Plan:
             raise ValueError(f"plane must be a row-major ({self.ndm}, {self.nsamples}) {pdt} tensor on {data.device}")
         check(lib().pu_plan_dedisperse(self._h, ptr(data), data.stride(0), ptr(plane), plane.stride(0),
                                        stream_ptr(stream)), "pu_plan_dedisperse")
+        return plane
+
+    def dm_tiles(self):
+        """The plan's DM tiles in launch order: int32 arrays (first trial, trial count)."""
+        nt = int(self.info["dm_tiles"])
+        first, count = np.zeros(nt, np.int32), np.zeros(nt, np.int32)
+        lib().pu_plan_dm_tiles(self._h, first.ctypes.data_as(ctypes.c_void_p), count.ctypes.data_as(ctypes.c_void_p),
+                               nt)
+        return first, count
+
+    def dedisperse_dm_tile(self, data, dt, stream=None):
+        """Rows of DM tile ``dt``'s trials (``dm_tiles()[0][dt]`` onwards), shape (count,
+        nsamples), computed by the same kernel, tables and tiling as a full launch."""
+        t = torch()
+        self._check_data(data)
+        data = self._rows_aligned(data, stream)
+        first, count = self.dm_tiles()
+        if not 0 <= int(dt) < first.size:
+            raise ValueError(f"DM tile {dt} outside [0, {first.size})")
+        pdt = t.float64 if self.acc_is_f64 else t.float32
+        plane = t.empty((int(count[dt]), self.nsamples), dtype=pdt, device=data.device)
+        check(lib().pu_plan_dedisperse_dm_tile(self._h, ptr(data), data.stride(0), int(dt), ptr(plane),
+                                               plane.stride(0), stream_ptr(stream)), "pu_plan_dedisperse_dm_tile")
         return plane
 
 

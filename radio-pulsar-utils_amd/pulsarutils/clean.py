@@ -186,6 +186,20 @@ def get_noisier_channels(array):
     return spec > smooth_spec + 5 * ref_mad(spec)
 
 
+def moment_error_factor(n):
+    """Relative error bound of pu_row_moments' float64 sums of d and d^2 over a row of n.
+
+    The device sums each 8192-element block in a tree (depth <= 14 + 6), the trailing
+    partial block (up to 8191 elements) serially in rowsum_tail_kernel, and the block
+    sums one after another in moments_combine: a summation depth of at most
+    min(n, 8191) + ceil(n / 8192) + the block tree, plus the final combination
+    (V = s2 - 2 (m - c) s1 + n (m - c)^2, a few roundings).  A depth-h sum of
+    non-negative terms errs by <= h u of their total; the factor keeps 2^-40 as a floor
+    (the round-4 constant, exact-enough for n <= 8192)."""
+    depth = min(int(n), 8191) + -(-int(n) // 8192) + 64
+    return max(2.0 ** -40, depth * 2.0 ** -53)
+
+
 def _certified_variability(means, moments, n, acc_f32, badchans_mask):
     """measure_channel_variability's mask from one read pass, or None.
 
@@ -210,7 +224,7 @@ def _certified_variability(means, moments, n, acc_f32, badchans_mask):
     c, s1, s2 = mom[:, 0], mom[:, 1], mom[:, 2]
     dm = m - c
     V = s2 - 2.0 * dm * s1 + n * dm * dm
-    eV = (s2 + 2.0 * np.abs(dm) * np.sqrt(n * s2) + n * dm * dm) * 2.0 ** -40 + 1e-300
+    eV = (s2 + 2.0 * np.abs(dm) * np.sqrt(n * s2) + n * dm * dm) * moment_error_factor(n) + 1e-300
     u = 2.0 ** -24 if acc_f32 else 2.0 ** -53
     gam = (35 + -(-n // 8192) + 4) * u
     s_lo = np.sqrt(np.maximum(V - eV, 0.0) * (1.0 - gam) / n * (1.0 - u)) * (1.0 - u)

@@ -363,7 +363,10 @@ def test_default_group_cost_model(gpu, golden, name, group, tile):
     plan = _hip.Plan(code, _hip.PU_ACC_NATIVE, c.nchan, c.nsamples, sh)
     assert plan.info["group"] == group and plan.info["trials_per_tile"] == tile, plan.info
     if name == "C3":
-        return  # C3's default-plan rows are checked bit-exact in test_search_c3_full_size_u8
+        # C3's production plan (5000 trials, tall G = 8): test_search_c3_full_size_u8 checks
+        # rows of its DM tile that holds the best trial bit-exact, through that plan itself
+        # (pu_plan_dedisperse_dm_tile: same instantiation, tables and tiling)
+        return
     xd = synth.pulsar_filterbank_device(c)
     plane = plan.dedisperse(xd)
     idx = np.array([0, dms.size // 3, dms.size - 1])
@@ -404,23 +407,31 @@ def test_plan_cache_reuse(gpu):
 
 def test_search_c3_full_size_u8(gpu):
     """Maximum size (C3: 4096 x 2^22 uint8, 5000 trials, 17 GB in HBM): the full search
-    finds the injected pulse; for the first, best and last trial the dedispersed series
-    is bit-equal to the float64 C oracle (integer partial sums < 2^24 are exact in float32)
-    and the statistics match it within SURVEY §8a's 1e-5."""
+    finds the injected pulse; the production plan's own rows - the DM tile that holds the
+    best trial, dedispersed by that plan (pu_plan_dedisperse_dm_tile: the tall G = 8
+    instantiation, slot/stage/window tables and tiling of the 5000-trial search) - are
+    bit-equal to the float64 C oracle for the tile's first, best and last trial (integer
+    partial sums < 2^24 are exact in float32), and the statistics match it within SURVEY
+    §8a's 1e-5."""
     import torch
     from pulsarutils import synth
     c = CONFIGS["C3"]
     xd = synth.pulsar_filterbank_device(c)
     dms = D.dedispersion_plan(c.nchan, c.dmmin, c.dmmax, c.start_freq, c.bandwidth, c.tsamp)
     assert dms.size == 5000
-    (mx, sd, snr, win), _ = D.search_device(xd, dms, c.nchan, c.start_freq, c.bandwidth, c.tsamp)
+    (mx, sd, snr, win), plan = D.search_device(xd, dms, c.nchan, c.start_freq, c.bandwidth, c.tsamp)
     torch.cuda.synchronize()
+    assert plan.info["group"] == 8 and plan.info["trials_per_tile"] == 256 and plan.ndm == 5000, plan.info
     snr = snr.cpu().numpy()
     best = int(np.argmax(snr))
     assert abs(dms[best] - c.pulse_dm) < 0.5, (dms[best], c.pulse_dm)
-    idx = np.array([0, best, dms.size - 1])
-    sh = _hip.shift_table(c.nchan, dms[idx], c.start_freq, c.bandwidth, c.tsamp)
-    plane = _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, c.nchan, c.nsamples, sh).dedisperse(xd).cpu().numpy()
+    first, count = plan.dm_tiles()
+    assert int(count.sum()) == dms.size and np.array_equal(np.sort(first), np.cumsum(np.r_[0, count[np.argsort(first)]])[:-1])
+    dt = int(np.nonzero((first <= best) & (best < first + count))[0][0])
+    rows = plan.dedisperse_dm_tile(xd, dt)
+    idx = np.array([int(first[dt]), best, int(first[dt] + count[dt] - 1)])
+    plane = rows[torch.as_tensor(idx - int(first[dt]), device=rows.device)].cpu().numpy()
+    del rows
     x = xd.cpu().numpy()
     del xd
     torch.cuda.empty_cache()
@@ -534,3 +545,36 @@ def test_default_group_ragged_vs_oracle(gpu, dt):
         pf = _plane(x, sh, "native", forced)
         if dt == "u8":
             np.testing.assert_array_equal(pf, plane)
+
+
+@pytest.mark.parametrize("dt,acc,group", [("f32", "native", 0), ("u8", "native", 8), ("f32", "f64", 1),
+                                          ("f64", "native", 1), ("f32", "native", 4)])
+def test_dedisperse_dm_tile_equals_full_plane(gpu, dt, acc, group):
+    """pu_plan_dedisperse_dm_tile: every DM tile's rows equal the full plane's rows of the
+    same trials bit for bit (subband and channel mode, sorted tile orders included), and
+    the tiles cover the grid exactly once."""
+    import torch
+    c = CONFIGS["C2"]
+    rng = np.random.default_rng(52)
+    nchan, n = 96, 12000
+    x = rng.random((nchan, n)) * 50
+    x = {"f32": x.astype(np.float32), "u8": x.astype(np.uint8), "f64": x}[dt]
+    dms = np.linspace(0.0, 300.0, 333)
+    sh = _hip.shift_table(nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
+    code = {"u8": _hip.PU_U8, "f32": _hip.PU_F32, "f64": _hip.PU_F64}[dt]
+    accc = {"native": _hip.PU_ACC_NATIVE, "f64": _hip.PU_ACC_F64}[acc]
+    plan = _hip.Plan(code, accc, nchan, n, sh, group=group)
+    xd = _hip.to_device(x)
+    full = plan.dedisperse(xd)
+    first, count = plan.dm_tiles()
+    assert first.size == plan.info["dm_tiles"] and first.size > 1
+    seen = np.zeros(dms.size, int)
+    for t in range(first.size):
+        rows = plan.dedisperse_dm_tile(xd, t)
+        assert rows.shape == (int(count[t]), n)
+        assert torch.equal(rows, full[int(first[t]):int(first[t] + count[t])]), t
+        seen[first[t]:first[t] + count[t]] += 1
+    assert np.all(seen == 1)
+    with pytest.raises(ValueError):
+        _hip.check(_hip.lib().pu_plan_dedisperse_dm_tile(plan._h, _hip.ptr(xd), xd.stride(0), first.size,
+                                                         _hip.ptr(full), full.stride(0), None), "dm_tile")

@@ -82,3 +82,43 @@ def test_certified_variability_nonfinite_and_too_few_good():
     bad = np.ones(16, bool)
     bad[:4] = False  # 4 good channels: the reference's quartile index 12 raises
     assert _certified_variability(y.mean(1), _moments(y), 100, True, bad) is None
+
+
+@pytest.mark.parametrize("k", [0, 1, 3, 40])
+def test_moment_error_bound_covers_serial_tail(k):
+    """pu_row_moments sums a row's trailing partial block (up to 8191 elements)
+    serially and then the per-block sums one after another, so the float64 summation depth
+    reaches min(n, 8191) + ceil(n / 8192) + the block tree.  At n = 8192 k + 8191 the
+    bound's factor must cover that depth, and the rounding error of V formed the device's
+    way (blocks as pairwise trees, the tail and the block combine as serial chains) must lie
+    inside the bound eV _certified_variability uses."""
+    from fractions import Fraction
+    from pulsarutils.clean import moment_error_factor
+    n = 8192 * k + 8191
+    depth = min(n, 8191) + -(-n // 8192)
+    assert moment_error_factor(n) >= depth * 2.0 ** -53
+    rng = np.random.default_rng(70 + k)
+    x = (1000.0 + rng.normal(0.0, 3.0, n)).astype(np.float32).astype(np.float64)
+    c = x[0]
+    d = x - c
+    # the device's order: full blocks by a tree (numpy's pairwise sum here), the tail and the
+    # combine as serial float64 chains
+    nfull = n // 8192
+    blocks1 = [float(np.sum(d[b * 8192:(b + 1) * 8192])) for b in range(nfull)]
+    blocks2 = [float(np.sum(d[b * 8192:(b + 1) * 8192] ** 2)) for b in range(nfull)]
+    t1 = t2 = 0.0
+    for v in d[nfull * 8192:]:
+        t1 += float(v)
+        t2 += float(v) * float(v)
+    s1 = s2 = 0.0
+    for a, b in zip(blocks1 + [t1], blocks2 + [t2]):
+        s1 += a
+        s2 += b
+    m = float(np.mean(x))
+    dm = m - c
+    V = s2 - 2.0 * dm * s1 + n * dm * dm
+    exact_d = [Fraction(float(v)) for v in d]
+    S1, S2 = sum(exact_d), sum(v * v for v in exact_d)
+    Vx = S2 - 2 * Fraction(dm) * S1 + n * Fraction(dm) ** 2
+    eV = (s2 + 2.0 * abs(dm) * np.sqrt(n * s2) + n * dm * dm) * moment_error_factor(n)
+    assert abs(Fraction(V) - Vx) <= Fraction(eV)
