@@ -4,16 +4,20 @@ One "step" = one fused DM-trial search (pu_plan_search: shift-and-sum over all
 channels for every trial + the S/N epilogue + the per-trial finalize) over a
 1024-channel x 2^20-sample float32 filterbank resident in HBM, 1000 trials per GPU.
 
-Scaling (one process per GPU, torchrun; DM trials are independent, so there is no
-collective on the data path - DESIGN.md §5):
-* ``--scaling weak`` (default): the DM grid is N x ``ntrials`` trials, rank r owns
-  trials [r ntrials, (r+1) ntrials).
-* ``--scaling strong``: the config's own grid (C3: 5000 trials) is split contiguously
-  over the N ranks (C3 at N = 8: 625 trials per GPU).
-The filterbank is generated on rank 0 and RCCL-broadcast over xGMI before timing
-(``broadcast_ms``; chunked so the search of early time chunks overlaps the transfer
-of later ones: ``end_to_end_ms`` = broadcast + search of one step, pipelined); each
-step ends with an all_gather of the per-trial statistics.
+Scaling (one process per GPU, torchrun; DM trials are independent: the one exchange on
+the data path is the filterbank's distribution from rank 0 - DESIGN.md §5):
+* N = 1 (default): C2, 1000 trials, the filterbank resident in HBM.
+* N > 1 (default): BASELINE.json configs[2] as stated - C3 (4096 chan x 2^22 uint8,
+  17.2 GB) held by rank 0, its 5000 trials split contiguously over the N ranks
+  (``--scaling strong``; C3 at N = 8: 625 trials per GPU).  One timed step is the whole
+  job: the filterbank distributed from rank 0 in time chunks (``--collective``,
+  default scatter + all-gather over the xGMI mesh) with each rank's search of the time
+  tiles whose rows have landed overlapping the later chunks, the finalize, and the
+  all_gather of the per-trial (max, std, snr, rebin).  ``value`` = 5000 x 2^22 / step.
+* ``--scaling weak``: the DM grid is N x ``ntrials`` trials of ``--config`` (C2), rank r
+  owns trials [r ntrials, (r+1) ntrials); the filterbank is distributed before timing.
+``multi_gpu`` (N > 1) reports the whole-filterbank exchange alone and one pipelined
+step per collective (``broadcast`` and ``scatter_allgather``).
 
 Prints ONE JSON line (rank 0) with the driver's contract fields plus ``roofline``
 (dominant kernel, HIP events on its launch stream; HBM counter traffic from the PMC
@@ -39,7 +43,7 @@ import torch.distributed as dist  # noqa: E402
 from pulsarutils import _hip, synth  # noqa: E402
 from pulsarutils.configs import CONFIGS  # noqa: E402
 from pulsarutils.dedispersion import dedispersion_plan  # noqa: E402
-from pulsarutils.parallel import shard_bounds  # noqa: E402
+from pulsarutils.parallel import pipelined_broadcast_search, shard_bounds  # noqa: E402
 
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
 HBM_PEAK_GBS = 8000.0
@@ -293,14 +297,55 @@ def c3_strong(dev, world, rank, steps, chunks):
     return res
 
 
+def exchange_bench(x, plan, outs, ws, dev, chunks):
+    """N > 1: the whole filterbank distributed from rank 0 by each collective alone
+    (``*_ms``, ``*_GBps`` = bytes / time), then one pipelined step per collective (chunked
+    exchange + the search of each time tile as soon as its rows and halo landed +
+    finalize: ``end_to_end_ms``).  Barrier + sync on both sides, max over ranks."""
+    from pulsarutils.parallel import COLLECTIVES, broadcast_filterbank, pipelined_broadcast_search
+
+    def timed(fn):
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        ms = torch.tensor([(time.perf_counter() - t0) * 1e3], dtype=torch.float64, device=dev)
+        dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+        return round(float(ms.item()), 3)
+
+    nbytes = x.numel() * x.element_size()
+    res = {"bytes": nbytes, "bcast_chunks": chunks, "end_to_end_ms": {},
+           "what": "<collective>_ms: the whole filterbank from rank 0 by that exchange alone; end_to_end_ms: one "
+                   "chunked exchange pipelined with the search (each time tile launched once its rows and halo "
+                   "landed) and the finalize"}
+    for c in COLLECTIVES:
+        timed(lambda: broadcast_filterbank(x, src=0, collective=c))  # warm-up (communicator setup)
+        ms = timed(lambda: broadcast_filterbank(x, src=0, collective=c))
+        res[f"{c}_ms"] = ms
+        res[f"{c}_GBps"] = round(nbytes / ms / 1e6, 1)
+    for c in COLLECTIVES:
+        res["end_to_end_ms"][c] = timed(lambda: pipelined_broadcast_search(x, plan, outs, ws, src=0, chunks=chunks,
+                                                                          collective=c))
+    res["search_only_ms"] = timed(lambda: plan.search(x, out=outs, workspace=ws))
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="C2")
+    ap.add_argument("--config", default=None, help="default: C2 on one GPU, C3 (configs[2]) on N > 1")
     ap.add_argument("--acc", default="native", choices=["native", "f32", "f64"])
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
+                    help="default: weak (one GPU: the single-GPU workload), strong on N > 1")
+    ap.add_argument("--collective", default="scatter_allgather", choices=["broadcast", "scatter_allgather"],
+                    help="N > 1: the chunk exchange inside the timed strong-scaling step")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse the N > 1 path with every rank on the visible GPU(s), round robin "
+                         "(RCCL refuses two ranks on one device); timings are then not the product's")
     ap.add_argument("--shard", type=int, default=0,
                     help="with --scaling strong on one GPU: search only rank 0's slice of an N-way split "
                          "(e.g. --config C3 --scaling strong --shard 8: the 625-trial shard of the 8-GPU run)")
@@ -328,13 +373,22 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.scaling is None:
+        args.scaling = "strong" if world > 1 else "weak"
+    if args.config is None:
+        args.config = "C3" if world > 1 and args.scaling == "strong" else "C2"
     if args.gpus != world and world != 1:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}")
+    if args.dist_backend == "gloo":
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
 
     cfg = CONFIGS[args.config]
     if args.scaling == "weak":
@@ -374,42 +428,34 @@ def main():
             torch.empty(per_rank, dtype=torch.float64, device=dev),
             torch.empty(per_rank, dtype=torch.float64, device=dev),
             torch.empty(per_rank, dtype=torch.int32, device=dev))
-    local_stats = torch.zeros((3, chunk), dtype=torch.float64, device=dev)
-    gathered = torch.empty((world, 3, chunk), dtype=torch.float64, device=dev)
+    local_stats = torch.zeros((4, chunk), dtype=torch.float64, device=dev)
+    gathered = torch.empty((world, 4, chunk), dtype=torch.float64, device=dev)
 
     bcast = None
+    pipelined = world > 1 and args.scaling == "strong"
     if world > 1:
-        from pulsarutils.parallel import pipelined_broadcast_search
-        # broadcast alone (plain RCCL broadcast of the whole filterbank), then the
-        # chunked broadcast with the search of early time chunks overlapping it
-        dist.barrier()
-        torch.cuda.synchronize()
-        tb = time.perf_counter()
-        dist.broadcast(x, src=0)
-        torch.cuda.synchronize()
-        bcast_ms = (time.perf_counter() - tb) * 1e3
-        dist.barrier()
-        torch.cuda.synchronize()
-        tb = time.perf_counter()
-        pipelined_broadcast_search(x, plan, outs, ws, src=0, chunks=args.bcast_chunks)
-        torch.cuda.synchronize()
-        e2e = torch.tensor([(time.perf_counter() - tb) * 1e3], dtype=torch.float64, device=dev)
-        dist.all_reduce(e2e, op=dist.ReduceOp.MAX)
-        bcast = {"broadcast_ms": bcast_ms, "broadcast_GBps": x.numel() * x.element_size() / bcast_ms / 1e6,
-                 "end_to_end_ms": float(e2e.item()), "bcast_chunks": args.bcast_chunks,
-                 "what": "end_to_end_ms: chunked RCCL broadcast of the filterbank + the search of one step, "
-                         "the search of each time chunk launched as soon as its rows (and halo) landed"}
+        bcast = exchange_bench(x, plan, outs, ws, dev, args.bcast_chunks)
+        if rank == 0:
+            log(f"exchange {bcast}")
 
     def step():
-        plan.search(x, out=outs, workspace=ws)
+        if pipelined:
+            # the whole job: rank 0's filterbank distributed in time chunks, every rank
+            # searching the tiles whose rows have landed, then the finalize
+            pipelined_broadcast_search(x, plan, outs, ws, src=0, chunks=args.bcast_chunks,
+                                       collective=args.collective)
+        else:
+            plan.search(x, out=outs, workspace=ws)
         if world > 1:
-            local_stats[:, :per_rank].copy_(torch.stack(outs[:3]))
+            local_stats[:, :per_rank].copy_(torch.stack([outs[0], outs[1], outs[2], outs[3].to(torch.float64)]))
             dist.all_gather_into_tensor(gathered, local_stats)
 
     for i in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    plan.enable_timing(args.steps)
+    # a pipelined step launches the search once per run of landed time tiles
+    nslots = args.steps * (4 * args.bcast_chunks + 4 if pipelined else 1)
+    plan.enable_timing(nslots)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -420,7 +466,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kms = plan.kernel_times_ms(args.steps)
+    kms = plan.kernel_times_ms(nslots)
     cert = plan.cert_info()
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -439,7 +485,8 @@ def main():
 
     total_samples = dms_all.size * cfg.nsamples
     value = total_samples / (ms_per_step / 1e3)
-    kernel_ms = float(np.mean(kms)) if len(kms) else None
+    # kernel time per step (pipelined: the sum of the step's tile-range launches)
+    kernel_ms = float(np.sum(kms)) / args.steps if len(kms) else None
     adds = float(cfg.nchan) * cfg.nsamples * per_rank
     esz = {"f32": 4, "u8": 1, "f64": 8}[cfg.dtype]
     alg_bytes = float(cfg.nchan) * cfg.nsamples * esz  # compulsory input read per launch (stats mode)
@@ -506,7 +553,7 @@ def main():
         log(f"cpu baseline {cpu['value']:.3e} samples/s on {threads} threads ({cpu['cpu_model']})")
 
     c3 = None
-    if not args.no_c3_strong and args.config != "C3":
+    if not args.no_c3_strong and args.config != "C3" and world == 1:
         del x, ws, outs, plan
         torch.cuda.empty_cache()
         log("c3_strong ...")
@@ -521,17 +568,22 @@ def main():
                 "vs_baseline": None,
                 "dtype": {"f32": "f32", "u8": "u8", "f64": "f64"}[cfg.dtype] + ("" if args.acc == "native"
                                                                                  else f"(acc {args.acc})"),
-                "data": "synthetic (noise + unit pulse at DM %g, generated in HBM)" % cfg.pulse_dm,
+                "data": "synthetic (noise + unit pulse at DM %g, generated in HBM%s)" % (
+                    cfg.pulse_dm, " of rank 0 and distributed inside every timed step" if pipelined else ""),
                 "config": {"workload": f"{cfg.name}: {cfg.nchan} chan x 2^{int(np.log2(cfg.nsamples))} "
                                       f"{cfg.dtype} samples, {dms_all.size} DM trials "
                                       f"({'per GPU' if args.scaling == 'weak' else 'in all'})",
                            "nchan": cfg.nchan, "nsamples": cfg.nsamples, "trials_per_gpu": per_rank,
                            "total_trials": int(dms_all.size), "parallelism": f"dm-shard{world}",
                            "best_dm": best_dm},
+                "step": ("chunked filterbank exchange from rank 0 (%s) pipelined with each rank's search of its "
+                         "DM slice, finalize, all_gather of (max, std, snr, rebin)" % args.collective
+                         if pipelined else "pu_plan_search of the resident filterbank" +
+                         (" + all_gather of (max, std, snr, rebin)" if world > 1 else "")),
                 "roofline": roof, "clean": clean, "cpu_baseline": cpu,
                 "certify": dict(cert, what="trials of the last timed step whose fast statistics could not be "
                                            "certified and were recomputed exactly (DESIGN.md §4.5)"),
-                "env": knobs, "valid": not knobs}
+                "env": knobs, "valid": not knobs and args.dist_backend == "nccl"}
         if f64 is not None:
             line["acc_f64"] = f64
         if c3 is not None:

@@ -3,11 +3,15 @@
 The reference's only parallelism is numba ``prange`` over independent DM trials
 (``dedispersion.py:174,181``).  Here the same trial axis is split across ranks:
 
-1. the filterbank is broadcast from ``src`` (RCCL over xGMI; the data path of the
+1. the filterbank is distributed from ``src`` (RCCL over xGMI; the data path of the
    search itself has no other exchange).  :func:`pipelined_broadcast_search` cuts the
-   broadcast into time chunks and starts the search of each time tile as soon as the
+   transfer into time chunks and starts the search of each time tile as soon as the
    columns it reads (its window plus the shift halo) have landed, so the transfer of
-   later chunks overlaps the search of earlier ones;
+   later chunks overlaps the search of earlier ones.  Two exchanges per chunk
+   (``collective``): ``"broadcast"`` (one RCCL broadcast from ``src``) or
+   ``"scatter_allgather"`` (``src`` scatters 1/world of the chunk to every rank, then all
+   ranks all-gather it: the second step's traffic runs over every xGMI link of the mesh
+   instead of leaving ``src``'s links alone; SURVEY §8e, DESIGN §5);
 2. each rank searches its contiguous slice of the trial grid on its own GPU,
 3. the per-trial statistics (max, std, snr, rebin) are all-gathered, so every rank
    ends with the reference's full-length result arrays.
@@ -31,10 +35,29 @@ def _hip_compute(data, dms, nchan, start_freq, bandwidth, sample_time, acc):
     return mx, sd, snr, win.to(mx.dtype)
 
 
-def broadcast_filterbank(data, src=0, group=None):
-    """Broadcast the (nchan, N) filterbank tensor from ``src`` to every rank, in place."""
+def broadcast_filterbank(data, src=0, group=None, collective="broadcast"):
+    """Give every rank ``src``'s (nchan, N) filterbank tensor, in place (contiguous data:
+    the whole tensor is one :func:`exchange_chunk`; a padded tail goes through a staging
+    copy when ``scatter_allgather`` needs a multiple of world elements)."""
+    import torch
     import torch.distributed as dist
-    dist.broadcast(data, src=src, group=group)
+    if collective == "broadcast":
+        dist.broadcast(data, src=src, group=group)
+        return data
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    flat = data.reshape(-1) if data.is_contiguous() else None
+    blen = -(-data.numel() // world) * world
+    if flat is None or blen != data.numel():
+        staging = torch.empty(blen, dtype=data.dtype, device=data.device)
+        if rank == src:
+            staging[:data.numel()].copy_(data.reshape(-1))
+        exchange_chunk(staging, torch.empty(blen // world, dtype=data.dtype, device=data.device), rank, src,
+                       world, group, collective)
+        if rank != src:
+            data.copy_(staging[:data.numel()].view(data.shape))
+        return data
+    exchange_chunk(flat, torch.empty(blen // world, dtype=data.dtype, device=data.device), rank, src, world,
+                   group, collective)
     return data
 
 
@@ -45,6 +68,31 @@ def column_chunks(nsamples, chunks, quantum=1024):
     n = int(nsamples)
     width = max(quantum, -(-(-(-n // max(1, int(chunks)))) // quantum) * quantum)
     return [(c0, min(n, c0 + width)) for c0 in range(0, n, width)]
+
+
+COLLECTIVES = ("broadcast", "scatter_allgather")
+
+
+def exchange_chunk(buf, piece, rank, src, world, group=None, collective="broadcast"):
+    """Make every rank's ``buf`` (1-D, contiguous) equal ``src``'s.
+
+    ``"broadcast"``: one broadcast from ``src``.  ``"scatter_allgather"``: ``buf``'s length
+    is a multiple of ``world``; ``src`` scatters piece r of it to rank r (into ``piece``, a
+    separate buffer of len(buf) / world elements) and every rank all-gathers the pieces
+    into ``buf``.  On ``src`` the all-gather rewrites ``buf`` with its own bytes."""
+    import torch.distributed as dist
+    if collective == "broadcast" or world == 1:
+        dist.broadcast(buf, src=src, group=group)
+        return buf
+    if collective != "scatter_allgather":
+        raise ValueError(f"collective must be one of {COLLECTIVES}, got {collective!r}")
+    m = buf.numel() // world
+    if m * world != buf.numel() or piece.numel() != m:
+        raise ValueError(f"scatter_allgather: buffer of {buf.numel()} elements is not {world} pieces of "
+                         f"{piece.numel()}")
+    dist.scatter(piece, list(buf.split(m)) if rank == src else None, src=src, group=group)
+    dist.all_gather_into_tensor(buf, piece, group=group)
+    return buf
 
 
 def ready_tiles(plan, landed):
@@ -99,11 +147,12 @@ def _masked_stream(reserve, dev):
 
 
 def pipelined_broadcast_search(data, plan, out=None, workspace=None, src=0, chunks=8, group=None, searcher=None,
-                               reserve_cus=0):
-    """Broadcast ``data`` from ``src`` in time chunks while searching it with ``plan``.
+                               reserve_cus=0, collective="broadcast"):
+    """Distribute ``data`` from ``src`` in time chunks while searching it with ``plan``.
 
     Chunk k (a range of whole time tiles, all channels) is packed into a contiguous
-    staging buffer on ``src``, broadcast (RCCL on a communication stream) and unpacked
+    staging buffer on ``src``, exchanged (RCCL on a communication stream; ``collective``:
+    :func:`exchange_chunk`'s broadcast or scatter + all-gather) and unpacked
     into ``data`` on the other ranks; every time tile whose read window has landed is
     searched (on a compute stream) as soon as its chunk's event fires
     (pu_plan_search_tiles), and the per-trial outputs are finalised when all tiles ran
@@ -153,17 +202,26 @@ def pipelined_broadcast_search(data, plan, out=None, workspace=None, src=0, chun
         cur = comm = comp = None
     on_comm = (lambda: torch.cuda.stream(comm)) if cuda else contextlib.nullcontext
     done = np.zeros(searcher.ntiles, dtype=bool) if searcher is not None else None
+    if collective not in COLLECTIVES:
+        raise ValueError(f"collective must be one of {COLLECTIVES}, got {collective!r}")
     width = max(c1 - c0 for c0, c1 in bounds)
-    staging = torch.empty(nchan * width, dtype=data.dtype, device=dev) if world > 1 else None
+    # staging holds whole chunks padded to a multiple of world elements (scatter pieces)
+    slen = -(-nchan * width // world) * world
+    staging = torch.empty(slen, dtype=data.dtype, device=dev) if world > 1 else None
+    piece = (torch.empty(slen // world, dtype=data.dtype, device=dev)
+             if world > 1 and collective == "scatter_allgather" else None)
     for k, (c0, c1) in enumerate(bounds):
         # tiles launched while later chunks are in flight use the masked stream
         tstream = masked.stream if masked is not None and k + 1 < len(bounds) else comp
         with on_comm():
             if world > 1:
-                buf = staging[:nchan * (c1 - c0)].view(nchan, c1 - c0)  # contiguous
+                blen = -(-nchan * (c1 - c0) // world) * world
+                flat = staging[:blen]
+                buf = flat[:nchan * (c1 - c0)].view(nchan, c1 - c0)  # contiguous
                 if rank == src:
                     buf.copy_(data[:, c0:c1])
-                dist.broadcast(buf, src=src, group=group)
+                exchange_chunk(flat, piece[:blen // world] if piece is not None else None, rank, src, world,
+                               group=group, collective=collective)
                 if rank != src:
                     data[:, c0:c1].copy_(buf)
             ev = None
@@ -185,6 +243,8 @@ def pipelined_broadcast_search(data, plan, out=None, workspace=None, src=0, chun
     if cuda:
         if staging is not None:
             staging.record_stream(comm)
+        if piece is not None:
+            piece.record_stream(comm)
         cur.wait_stream(comm)
     if searcher is None:
         return None
@@ -201,13 +261,14 @@ def pipelined_broadcast_search(data, plan, out=None, workspace=None, src=0, chun
 
 
 def sharded_search(data, trial_DMs, nchan, start_freq, bandwidth, sample_time, group=None, acc=None,
-                   compute=None, broadcast=True, src=0, pipelined=False, chunks=8):
+                   compute=None, broadcast=True, src=0, pipelined=False, chunks=8, collective="broadcast"):
     """Distributed ``_dedispersion_search``: returns (max, std, snr, rebin[int32]) numpy arrays
     covering ALL trials, on every rank.
 
     ``data`` must be a tensor of the right shape/dtype on every rank (only ``src``'s
     content matters when ``broadcast``).  ``pipelined`` (HIP compute only) overlaps the
-    broadcast with the search (:func:`pipelined_broadcast_search`).
+    transfer with the search (:func:`pipelined_broadcast_search`); ``collective`` picks
+    the transfer (:func:`exchange_chunk`: ``"broadcast"`` or ``"scatter_allgather"``).
     """
     import torch
     import torch.distributed as dist
@@ -231,7 +292,7 @@ def sharded_search(data, trial_DMs, nchan, start_freq, bandwidth, sample_time, g
                              _acc_code(acc), ("dm-shard", sub.tobytes(), float(start_freq), float(bandwidth),
                                               float(sample_time)))
         if broadcast and world > 1:
-            res = pipelined_broadcast_search(x, plan, src=src, chunks=chunks, group=group)
+            res = pipelined_broadcast_search(x, plan, src=src, chunks=chunks, group=group, collective=collective)
         else:
             res = plan.search(x) if plan is not None else None
         if res is not None:
@@ -239,7 +300,7 @@ def sharded_search(data, trial_DMs, nchan, start_freq, bandwidth, sample_time, g
                 local[k, :hi - lo] = res[k].to(torch.float64)
     else:
         if broadcast and world > 1:
-            broadcast_filterbank(data, src=src, group=group)
+            broadcast_filterbank(data, src=src, group=group, collective=collective)
         fn = compute or (lambda d, t: _hip_compute(d, t, nchan, start_freq, bandwidth, sample_time, acc))
         if hi > lo:
             res = fn(data, dms[lo:hi])

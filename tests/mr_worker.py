@@ -1,6 +1,6 @@
 """One rank of tests/test_gpu_multirank.py (not collected by pytest: no ``test_`` prefix).
 
-    python tests/mr_worker.py RANK WORLD PORT CASE
+    python tests/mr_worker.py RANK WORLD PORT CASE [COLLECTIVE]
 
 Every rank runs on cuda:0 of the one leased GPU with a ``gloo`` process group (RCCL
 refuses two ranks on one device; gloo's CUDA broadcast / all_gather stage device
@@ -16,6 +16,8 @@ from garbage.  Checks (bit for bit):
     _dedispersion_search of each rank's trial slice (the same plans);
   * CASE C5m: the same with reserve_cus=8 (the CU-masked compute stream), outputs freed
     afterwards (the masked stream must outlive the tensors recorded on it).
+COLLECTIVE (default broadcast): the chunk exchange of parallel.exchange_chunk -
+``broadcast`` or ``scatter_allgather`` (the mesh variant, round 5).
 Prints ``RANK r OK`` and exits 0, or raises (non-zero exit, traceback on stderr).
 """
 import os
@@ -28,6 +30,7 @@ sys.path[:0] = [os.path.join(REPO, "radio-pulsar-utils_amd"), REPO]
 
 def main():
     rank, world, port, case = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
+    collective = sys.argv[5] if len(sys.argv) > 5 else "broadcast"
     from dataclasses import replace
 
     import numpy as np
@@ -59,7 +62,8 @@ def main():
     plan = _hip.Plan(_hip.dtype_code(x_ref.dtype), _hip.PU_ACC_NATIVE, c.nchan, c.nsamples, sh)
     ref = [o.cpu().numpy() for o in plan.search(x_ref)]
     x = received()
-    res = parallel.pipelined_broadcast_search(x, plan, src=src, chunks=chunks, reserve_cus=reserve)
+    res = parallel.pipelined_broadcast_search(x, plan, src=src, chunks=chunks, reserve_cus=reserve,
+                                              collective=collective)
     got = [o.cpu().numpy() for o in res]
     torch.cuda.synchronize()
     assert torch.equal(x, x_ref), f"rank {rank}: received filterbank differs"
@@ -72,7 +76,7 @@ def main():
     # ---- sharded search (each rank its trial slice, all_gather of the statistics)
     x2 = received()
     mx, sd, snr, win = parallel.sharded_search(x2, dms, c.nchan, c.start_freq, c.bandwidth, c.tsamp,
-                                               pipelined=True, src=src, chunks=chunks)
+                                               pipelined=True, src=src, chunks=chunks, collective=collective)
     torch.cuda.synchronize()
     assert torch.equal(x2, x_ref), f"rank {rank}: received filterbank differs (sharded)"
     parts = []
@@ -88,7 +92,7 @@ def main():
     assert ntrials < full.size or abs(dms[best] - c.pulse_dm) < 1.0, (dms[best], c.pulse_dm)
     dist.barrier()
     dist.destroy_process_group()
-    print(f"RANK {rank} OK case {case} world {world} best DM {dms[best]:.3f} snr {snr[best]:.3f}", flush=True)
+    print(f"RANK {rank} OK case {case} world {world} {collective} best DM {dms[best]:.3f} snr {snr[best]:.3f}", flush=True)
 
 
 if __name__ == "__main__":

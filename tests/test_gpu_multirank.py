@@ -26,12 +26,16 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,case", [(2, "C5"), (3, "C5"), (2, "C3s"), (3, "C3s"), (2, "C5m")])
-def test_multirank_pipelined_and_sharded_on_one_gpu(gpu, world, case):
+@pytest.mark.parametrize("world,case,collective", [
+    (2, "C5", "broadcast"), (3, "C5", "broadcast"), (2, "C3s", "broadcast"), (3, "C3s", "broadcast"),
+    (2, "C5m", "broadcast"),
+    # round 5: the mesh exchange (scatter 1/world of each chunk, then all-gather)
+    (2, "C5", "scatter_allgather"), (3, "C3s", "scatter_allgather"), (3, "C5m", "scatter_allgather")])
+def test_multirank_pipelined_and_sharded_on_one_gpu(gpu, world, case, collective):
     port = _free_port()
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="4")
     procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "mr_worker.py"), str(r), str(world), str(port),
-                               case], stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env)
+                               case, collective], stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env)
              for r in range(world)]
     outs = []
     try:

@@ -49,7 +49,7 @@ WORKER = textwrap.dedent("""
     def compute(d, t):
         return oracle.search(d.numpy(), t, h["fbottom"], h["bandwidth"], h["tsamp"], nthreads=1)
     mx, sd, snr, win = sharded_search(data, dms, arr.shape[0], h["fbottom"], h["bandwidth"], h["tsamp"],
-                                      compute=compute)
+                                      compute=compute, collective={collective!r})
     ref = oracle.search(arr, dms, h["fbottom"], h["bandwidth"], h["tsamp"], nthreads=1)
     assert np.array_equal(data.numpy(), arr)
     for a, b in zip((mx, sd, snr, win), ref):
@@ -61,10 +61,15 @@ WORKER = textwrap.dedent("""
 """)
 
 
-@pytest.mark.parametrize("world,ndm", [(2, 37), (2, 3), (3, 37), (3, 2), (4, 38), (4, 3)])
-def test_sharded_search_gloo(tmp_path, world, ndm):
+@pytest.mark.parametrize("world,ndm,collective", [(2, 37, "broadcast"), (2, 3, "scatter_allgather"),
+                                                   (3, 37, "scatter_allgather"), (3, 2, "broadcast"),
+                                                   (4, 38, "scatter_allgather"), (4, 3, "broadcast")])
+def test_sharded_search_gloo(tmp_path, world, ndm, collective):
+    """Both filterbank exchanges (broadcast; scatter + all-gather, with a tail padded to a
+    multiple of world at world 3) give every rank the source's data and the single-process
+    result."""
     script = tmp_path / "worker.py"
-    script.write_text(WORKER.format(pkg=PKG_DIR, repo=REPO, ndm=ndm))
+    script.write_text(WORKER.format(pkg=PKG_DIR, repo=REPO, ndm=ndm, collective=collective))
     port = _free_port()
     procs = []
     for rank in range(world):
@@ -172,7 +177,8 @@ PIPE_WORKER = textwrap.dedent("""
             return "finalized"
 
     s = CheckSearcher()
-    assert pipelined_broadcast_search(data, None, src={src}, chunks={chunks}, searcher=s) == "finalized"
+    assert pipelined_broadcast_search(data, None, src={src}, chunks={chunks}, searcher=s,
+                                      collective={collective!r}) == "finalized"
     assert np.array_equal(data.numpy(), full)
     dist.barrier()
     dist.destroy_process_group()
@@ -180,13 +186,14 @@ PIPE_WORKER = textwrap.dedent("""
 """)
 
 
+@pytest.mark.parametrize("collective", ["broadcast", "scatter_allgather"])
 @pytest.mark.parametrize("world,src,n,chunks,smin,smax,dtype", [
     (2, 0, 50000, 5, -2084, 2914, "float32"),
     (3, 1, 1 << 16, 8, 0, 582, "uint8"),
     (4, 3, 40962, 3, -843, 1931, "float64"),
     (2, 1, 9000, 8, 100, 700, "uint8"),
 ])
-def test_pipelined_broadcast_gloo(tmp_path, world, src, n, chunks, smin, smax, dtype):
+def test_pipelined_broadcast_gloo(tmp_path, world, src, n, chunks, smin, smax, dtype, collective):
     """The multi-rank branch of parallel.pipelined_broadcast_search (staging pack on the
     source, chunk broadcast, unpack on the others, ready-tile launches) on CPU under gloo
     at world 2-4 with any source rank: every time tile is searched exactly once, only
@@ -194,7 +201,7 @@ def test_pipelined_broadcast_gloo(tmp_path, world, src, n, chunks, smin, smax, d
     equals the source on every rank at the end."""
     script = tmp_path / "pipe_worker.py"
     script.write_text(PIPE_WORKER.format(pkg=PKG_DIR, repo=REPO, n=n, src=src, chunks=chunks, smin=smin, smax=smax,
-                                         dtype=dtype))
+                                         dtype=dtype, collective=collective))
     port = _free_port()
     procs = []
     for rank in range(world):
