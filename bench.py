@@ -286,8 +286,9 @@ def c3_strong(dev, world, rank, steps, chunks):
         chunk = -(-dms_all.size // world)
         loc = torch.full((chunk,), -1.0, dtype=torch.float64, device=dev)
         loc[:hi - lo] = snr
-        allv = torch.empty((world, chunk), dtype=torch.float64, device=dev)
+        allv = torch.empty(world * chunk, dtype=torch.float64, device=dev)
         dist.all_gather_into_tensor(allv, loc)
+        allv = allv.view(world, chunk)
         snr = torch.cat([allv[r, :shard_bounds(dms_all.size, world, r)[1] - shard_bounds(dms_all.size, world, r)[0]]
                          for r in range(world)])
     res["best_dm"] = float(dms_all[int(torch.argmax(snr).item())])
@@ -429,7 +430,7 @@ def main():
             torch.empty(per_rank, dtype=torch.float64, device=dev),
             torch.empty(per_rank, dtype=torch.int32, device=dev))
     local_stats = torch.zeros((4, chunk), dtype=torch.float64, device=dev)
-    gathered = torch.empty((world, 4, chunk), dtype=torch.float64, device=dev)
+    gathered = torch.empty((world * 4, chunk), dtype=torch.float64, device=dev)  # rank-major (4, chunk) blocks
 
     bcast = None
     pipelined = world > 1 and args.scaling == "strong"
@@ -476,7 +477,7 @@ def main():
 
     # spot check: best trial of the whole grid (rank 0's view of the gathered S/N)
     if world > 1:
-        snr_all = np.concatenate([gathered[r, 2, :shard_bounds(dms_all.size, world, r)[1]
+        snr_all = np.concatenate([gathered.view(world, 4, chunk)[r, 2, :shard_bounds(dms_all.size, world, r)[1]
                                            - shard_bounds(dms_all.size, world, r)[0]].cpu().numpy()
                                   for r in range(world)])
     else:
