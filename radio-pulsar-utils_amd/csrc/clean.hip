@@ -531,16 +531,17 @@ gauss_pair_kernel(const double *__restrict__ x, int64_t n, const double *__restr
 // order is scipy's: acc = x[i] w[r], then acc += (x[i+j] + x[i-j]) w[r+j], j = -r..-1.
 constexpr int kGaussQuadThreads = 256;
 
+// One workgroup's 4 T outputs [i0, i0 + 4 T) into a[4] (thread t: outputs i0 + 4 t + q).
+// gsm4: LDS of ((r + 2) & ~1) + 4 T + 2 r + 2 kGaussPad doubles.  Returns after the last
+// LDS read of the workgroup's staging only once every thread has passed the staging barrier
+// (callers that restage must __syncthreads() first).
 template <int T>
-__global__ void __launch_bounds__(T)
-gauss_quad_kernel(const double *__restrict__ x, int64_t n, const double *__restrict__ w, int r,
-                  double *__restrict__ out)
+__device__ __forceinline__ void gauss_quad_segment(const double *__restrict__ x, int64_t n, const double *__restrict__ w,
+                                                   int r, int64_t i0, double *gsm4, double (&a)[4])
 {
-    extern __shared__ __attribute__((aligned(16))) double gsm4[];
     const int wn = (r + 2) & ~1;  // weights padded to an even count: the window stays 16-B aligned
     double *ws = gsm4;
     double *xs = gsm4 + wn;       // x[i0 - r - pad, i0 + 1024 + r + pad), reflected at staging
-    const int64_t i0 = (int64_t)blockIdx.x * (4 * T);
     const int span = (4 * T) + 2 * r + 2 * kGaussPad;
     for (int k = threadIdx.x; k < wn; k += T) ws[k] = k <= r ? w[k] : 0.0;
     const int64_t g0 = i0 - r - kGaussPad;
@@ -554,13 +555,11 @@ gauss_quad_kernel(const double *__restrict__ x, int64_t n, const double *__restr
     }
     __syncthreads();
     const int t4 = 4 * (int)threadIdx.x;
-    const int64_t i = i0 + t4;
     // xc[q] = x[i + q]; xc + m is 16-B aligned whenever m + r is even (pad even, t4 even)
     const double *xc = xs + t4 + r + kGaussPad;
     auto pair = [&](int m) { return *reinterpret_cast<const f64x2 *>(xc + m); };
     auto wpair = [&](int m) { return *reinterpret_cast<const f64x2 *>(ws + r + m); };  // w[r+m], w[r+m+1]
     const double wr = ws[r];
-    double a[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) a[q] = xc[q] * wr;
     int j = -r;
@@ -604,6 +603,18 @@ gauss_quad_kernel(const double *__restrict__ x, int64_t n, const double *__restr
         a[2] += (l23.x + r23.x) * w0;
         a[3] += (l23.y + r23.y) * w0;
     }
+}
+
+template <int T>
+__global__ void __launch_bounds__(T)
+gauss_quad_kernel(const double *__restrict__ x, int64_t n, const double *__restrict__ w, int r,
+                  double *__restrict__ out)
+{
+    extern __shared__ __attribute__((aligned(16))) double gsm4[];
+    const int64_t i0 = (int64_t)blockIdx.x * (4 * T);
+    double a[4];
+    gauss_quad_segment<T>(x, n, w, r, i0, gsm4, a);
+    const int64_t i = i0 + 4 * (int)threadIdx.x;
     if (i + 3 < n && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
         *reinterpret_cast<f64x2 *>(out + i) = f64x2{a[0], a[1]};
         *reinterpret_cast<f64x2 *>(out + i + 2) = f64x2{a[2], a[3]};
@@ -1130,6 +1141,170 @@ __global__ void __launch_bounds__(256) median_final_kernel(MedState *st, const u
         out[0] = (0.0 + ((0.0 + a) + b)) / 2.0;
     } else {
         out[0] = (0.0 + (0.0 + a)) / 1.0;
+    }
+}
+
+// ---------------------------------------------------------------- light-curve factor
+// renormalize_data's 2^18-point chain in ONE launch (round 5; clean.py:77-82):
+//   lc_smooth = gaussian_filter(lc, sigma)      scipy's order (gauss_quad_segment)
+//   med = np.median(lc_smooth)                  the radix select above, six digit passes
+//   factor = med / lc_smooth                    as ratio_dev_kernel
+// Until round 4 these were 10 launches (Gaussian, median init + 6 histogram passes + final,
+// ratio).  Here each workgroup computes the Gaussian of its 1024-sample segments into LDS
+// and keeps them there; the select's digit passes histogram those LDS values and are
+// separated by grid barriers (a monotonic arrival counter: every histogram-adding wave's
+// vmcnt(0), the workgroup barrier, lane 0's agent release, the arrival, a relaxed poll with
+// s_sleep, the agent acquire - MI355X_MICROARCH.md, inter-workgroup visibility) instead of
+// kernel boundaries; the factor is written from the LDS values at the end.  Co-residency:
+// the grid is at most one workgroup per CU and a workgroup takes <= ~110 KB of LDS at the
+// largest supported n, so every workgroup of the grid is resident at once on the whole
+// device (the cleaning kernels never run on a CU-masked stream).
+// The histogram buffers rotate as in pu_median: pass p clears buffer (p + 1) % 3, whose last
+// reader was pass p - 1's select (before barrier p - 1); pass 5 clears buffer 0, so the
+// workspace leaves as it must enter (buffer 0 zero); the last workgroup out resets the
+// counters.
+constexpr int kLcThreads = 256;
+constexpr int kLcSeg = 4 * kLcThreads;  // Gaussian outputs per segment
+constexpr int kLcMaxSegs = 8;           // segments per workgroup kept in LDS (64 KB)
+
+struct LcState {
+    unsigned arrive;  // grid-barrier arrivals within a launch
+    unsigned leave;   // workgroups past the last barrier
+    unsigned nan;     // NaNs among the smoothed values
+    unsigned pad[61];
+};
+static_assert(sizeof(LcState) == 256, "LcState");
+
+__device__ __forceinline__ void lc_grid_barrier(LcState *st, unsigned target)
+{
+    asm volatile("s_waitcnt vmcnt(0)" : : : "memory");  // this wave's histogram atomics done
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
+        __hip_atomic_fetch_add(&st->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (__hip_atomic_load(&st->arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target)
+            __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
+    }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(kLcThreads)
+lc_factor_kernel(const double *__restrict__ lc, int64_t n, const double *__restrict__ w, int r, int segs,
+                 double *__restrict__ factor, double *__restrict__ med_out, LcState *st, uint32_t *hist)
+{
+    extern __shared__ __attribute__((aligned(16))) double lsm[];
+    const int gwords = ((r + 2) & ~1) + kLcSeg + 2 * r + 2 * kGaussPad;
+    double *vals = lsm;                                                  // [segs][kLcSeg]
+    double *gsm = lsm + segs * kLcSeg;                                   // Gaussian staging
+    uint32_t *h = reinterpret_cast<uint32_t *>(gsm + gwords);            // [2][kMedBins]
+    uint32_t *scan = h + 2 * kMedBins;                                   // [256]
+    int64_t *res = reinterpret_cast<int64_t *>(scan + kLcThreads);       // [2]
+    const int t = threadIdx.x;
+    const unsigned G = gridDim.x;
+    // 1. the smoothed values of segments blockIdx.x + G s
+    uint32_t nans = 0;
+    for (int sg = 0; sg < segs; ++sg) {
+        const int64_t i0 = ((int64_t)blockIdx.x + (int64_t)G * sg) * kLcSeg;
+        if (i0 >= n) break;  // uniform
+        double a[4];
+        gauss_quad_segment<kLcThreads>(lc, n, w, r, i0, gsm, a);
+        const int64_t i = i0 + 4 * t;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            vals[sg * kLcSeg + 4 * t + q] = a[q];
+            nans += (i + q < n && a[q] != a[q]) ? 1u : 0u;
+        }
+        __syncthreads();  // every thread is done with the staging before it is refilled
+    }
+    if (nans) atomicAdd(&st->nan, nans);
+    // 2. radix select of ranks k0 = n/2 - 1 (n even; n/2 odd) and k1 = n/2
+    uint64_t pfx[2] = {0, 0};
+    int64_t kk[2] = {(n % 2 == 0) ? n / 2 - 1 : n / 2, n / 2};
+    for (int pass = 0; pass < kMedPasses; ++pass) {
+        if (pass > 0) {
+            const uint32_t *hp = hist + (size_t)((pass - 1) % kMedBufs) * 2 * kMedBins;
+            for (int j = 0; j < 2; ++j) {
+                int bin;
+                int64_t rem;
+                med_select_block(hp + j * kMedBins, kk[j], scan, res, bin, rem);
+                pfx[j] |= (uint64_t)bin << med_shift(pass - 1);
+                kk[j] = rem;
+            }
+        }
+        uint32_t *nxt = hist + (size_t)((pass + 1) % kMedBufs) * 2 * kMedBins;
+        for (int i = blockIdx.x * kLcThreads + t; i < 2 * kMedBins; i += G * kLcThreads) nxt[i] = 0;
+        for (int i = t; i < 2 * kMedBins; i += kLcThreads) h[i] = 0;
+        __syncthreads();
+        const int shift = med_shift(pass), bits = med_bits(pass);
+        const uint64_t dmask = (uint64_t(1) << bits) - 1;
+        const int hs = shift + bits;  // bits above the digit must match the prefix
+        for (int sg = 0; sg < segs; ++sg) {
+            const int64_t i0 = ((int64_t)blockIdx.x + (int64_t)G * sg) * kLcSeg;
+            if (i0 >= n) break;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const double d = vals[sg * kLcSeg + 4 * t + q];
+                if (i0 + 4 * t + q >= n || d != d) continue;
+                const uint64_t k = order_key(d);
+                const uint32_t dig = (uint32_t)((k >> shift) & dmask);
+                if (hs >= 64 || (k >> hs) == (pfx[0] >> hs)) atomicAdd(&h[dig], 1u);
+                if (hs >= 64 || (k >> hs) == (pfx[1] >> hs)) atomicAdd(&h[kMedBins + dig], 1u);
+            }
+        }
+        __syncthreads();
+        uint32_t *cur = hist + (size_t)(pass % kMedBufs) * 2 * kMedBins;
+        for (int i = t; i < 2 * kMedBins; i += kLcThreads) {
+            const uint32_t c = h[i];
+            if (c) atomicAdd(&cur[i], c);
+        }
+        lc_grid_barrier(st, G * (unsigned)(pass + 1));
+    }
+    // 3. the last digit, numpy's mean of the two order statistics (NaN if any NaN), factor
+    {
+        const uint32_t *hp = hist + (size_t)((kMedPasses - 1) % kMedBufs) * 2 * kMedBins;
+        for (int j = 0; j < 2; ++j) {
+            int bin;
+            int64_t rem;
+            med_select_block(hp + j * kMedBins, kk[j], scan, res, bin, rem);
+            pfx[j] |= (uint64_t)bin << med_shift(kMedPasses - 1);
+        }
+    }
+    const bool any_nan = __hip_atomic_load(&st->nan, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    double med;
+    if (any_nan) {
+        med = __longlong_as_double(0x7ff8000000000000ll);
+    } else {
+        const double a = key_value(pfx[0]);
+        med = (n % 2 == 0) ? (0.0 + ((0.0 + a) + key_value(pfx[1]))) / 2.0 : (0.0 + (0.0 + a)) / 1.0;
+    }
+    if (blockIdx.x == 0 && t == 0 && med_out) med_out[0] = med;
+    for (int sg = 0; sg < segs; ++sg) {
+        const int64_t i0 = ((int64_t)blockIdx.x + (int64_t)G * sg) * kLcSeg;
+        if (i0 >= n) break;
+        const int64_t i = i0 + 4 * t;
+        if (i + 3 < n && (reinterpret_cast<uintptr_t>(factor) & 15) == 0) {
+            const double *v = vals + sg * kLcSeg + 4 * t;
+            *reinterpret_cast<f64x2 *>(factor + i) = f64x2{med / v[0], med / v[1]};
+            *reinterpret_cast<f64x2 *>(factor + i + 2) = f64x2{med / v[2], med / v[3]};
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (i + q < n) factor[i + q] = med / vals[sg * kLcSeg + 4 * t + q];
+        }
+    }
+    // 4. the last workgroup out resets the counters (every workgroup has passed every
+    // barrier and read the NaN count)
+    __syncthreads();
+    if (t == 0) {
+        const unsigned before = __hip_atomic_fetch_add(&st->leave, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (before == G - 1) {
+            __hip_atomic_store(&st->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&st->nan, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&st->leave, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -1690,6 +1865,74 @@ int pu_ratio_dev(const double *numerator, const double *x, int64_t n, double *ou
     hipLaunchKernelGGL(ratio_dev_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, pu::as_stream(stream), numerator, x,
                        n, out);
     return pu::launch_check("ratio_dev_kernel");
+}
+
+namespace {
+struct LcGeom {
+    bool fused;
+    int grid, segs;
+    size_t lds;
+};
+
+LcGeom lc_geom(int64_t n, int64_t r)
+{
+    LcGeom g{false, 0, 0, 0};
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return g;
+    if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return g;
+    if (r > kGaussMaxR || n <= 0 || cus[dev] <= 0) return g;
+    const int64_t nseg = (n + kLcSeg - 1) / kLcSeg;
+    g.grid = (int)std::min<int64_t>(nseg, cus[dev]);
+    g.segs = (int)((nseg + g.grid - 1) / g.grid);
+    const int64_t gwords = ((r + 2) & ~int64_t(1)) + kLcSeg + 2 * r + 2 * kGaussPad;
+    g.lds = (size_t)g.segs * kLcSeg * 8 + (size_t)gwords * 8 + 2 * kMedBins * 4 + kLcThreads * 4 + 16;
+    g.fused = g.segs <= kLcMaxSegs && g.lds <= 160 * 1024;
+    return g;
+}
+
+size_t lc_head_bytes() { return sizeof(LcState) + (size_t)kMedBufs * 2 * kMedBins * sizeof(uint32_t); }
+}  // namespace
+
+size_t pu_lc_factor_workspace_bytes(int64_t n)
+{
+    // fused: the state and the three histogram buffers; otherwise (r > kGaussMaxR or a very
+    // long series) also the smoothed series, pu_median's workspace and the median
+    const size_t head = lc_head_bytes();
+    return head + (((size_t)std::max<int64_t>(n, 0) * 8 + 255) & ~size_t(255)) + pu_median_workspace_bytes() + 64;
+}
+
+int pu_lc_factor(const double *lc, int64_t n, const double *w, int64_t r, double *factor, double *median_out, void *ws,
+                 size_t ws_bytes, void *stream)
+{
+    PU_REQUIRE(lc && w && factor && n > 0 && r >= 0, "pu_lc_factor: bad arguments");
+    PU_REQUIRE(ws && ws_bytes >= pu_lc_factor_workspace_bytes(n) && reinterpret_cast<uintptr_t>(ws) % 256 == 0,
+               "pu_lc_factor: workspace too small or not 256-byte aligned");
+    hipStream_t s = pu::as_stream(stream);
+    char *wsb = reinterpret_cast<char *>(ws);
+    const LcGeom g = lc_geom(n, r);
+    if (g.fused) {
+        static bool attr_set = false;
+        if (!attr_set) {
+            PU_TRY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(lc_factor_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+            attr_set = true;
+        }
+        LcState *st = reinterpret_cast<LcState *>(wsb);
+        uint32_t *hist = reinterpret_cast<uint32_t *>(st + 1);
+        hipLaunchKernelGGL(lc_factor_kernel, dim3(g.grid), dim3(kLcThreads), g.lds, s, lc, n, w, (int)r, g.segs, factor,
+                           median_out, st, hist);
+        return pu::launch_check("lc_factor_kernel");
+    }
+    // the launch-by-launch path: Gaussian, median, ratio
+    double *smooth = reinterpret_cast<double *>(wsb + lc_head_bytes());
+    char *mws = wsb + lc_head_bytes() + (((size_t)n * 8 + 255) & ~size_t(255));
+    double *med = reinterpret_cast<double *>(mws + pu_median_workspace_bytes());
+    int rc = pu_gaussian_filter1d(lc, n, w, r, smooth, stream);
+    if (!rc) rc = pu_median(smooth, n, median_out ? median_out : med, mws, pu_median_workspace_bytes(), stream);
+    if (!rc) rc = pu_ratio_dev(median_out ? median_out : med, smooth, n, factor, stream);
+    return rc;
 }
 
 int pu_zero_columns(double *out, int64_t nrows, int64_t ld, const int64_t *cols, int64_t ncols, void *stream)

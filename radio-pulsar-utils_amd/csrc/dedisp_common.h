@@ -508,13 +508,12 @@ __device__ __forceinline__ double swap16_combine_f64(double a, double b, Op op)
 // its own 6-step DPP chain (about 480 instructions per trial: the larger part of the C1
 // kernel).  All sums in float64 (<= 11 roundings per term: gamma = 2^-44 holds).
 // E = 1: lane l owns samples t0 + l + 64 k; E = 2: pairs t0 + 2 l + 128 j + {0, 1}.
-template <int E, int K>
-__device__ __forceinline__ void stats_full_f64(const double (&acc)[kD][K], const DedispArgs &a, int first, int slot0,
+template <int E, int K, int D = kD>
+__device__ __forceinline__ void stats_full_f64(const double (&acc)[D][K], const DedispArgs &a, int first, int slot0,
                                                int cnt, int tt, int lane)
 {
-    constexpr int D = kD;
     constexpr int NV = 9;  // sum y, sum of squares w = 1, 2, 4, 8, max w = 1, 2, 4, 8
-    static_assert(D == 8, "8 trials per wave");
+    static_assert(D == 8 || D == 4, "8 or 4 trials per wave");
     double kt;  // the tile mean of the wave's first trial (the shift of every record)
     {
         double s0 = acc[0][0];
@@ -605,11 +604,11 @@ __device__ __forceinline__ void stats_full_f64(const double (&acc)[kD][K], const
     const bool st_lane = rp == 0 ? (li <= 2 || li == 5 || li == 6 || li == 7 || li == 8 || li == 11 || li == 12)
                                  : (li == 3 || li == 4 || li == 9 || li == 10);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < D / 2; ++k) {
         double va[NV], vb[NV];
         lane_stats(k, va);
         __builtin_amdgcn_sched_barrier(0);
-        lane_stats(k + 4, vb);
+        lane_stats(k + D / 2, vb);
         double U[NV];
 #pragma unroll
         for (int i = 0; i < NV; ++i)
@@ -626,7 +625,7 @@ __device__ __forceinline__ void stats_full_f64(const double (&acc)[kD][K], const
         v = (li == 6 || li == 9) ? P1 : v;
         v = (li == 7 || li == 10) ? P4 : v;
         v = li == 12 ? P2 : v;
-        const int trial = row < 2 ? k : k + 4;
+        const int trial = row < 2 ? k : k + D / 2;
         if (st_lane && slot0 + trial < cnt)
             reinterpret_cast<double *>(a.partials)[((size_t)(first + slot0 + trial) * a.ntt + tt) * kPartStride + li] = v;
         __builtin_amdgcn_sched_barrier(0);

@@ -11,14 +11,18 @@
 
 #include "dedisp_common.h"
 
+// the state machine's entry labels (T0_0) are reached by falling through
+#pragma clang diagnostic ignored "-Wunused-label"
+
 namespace {
 
 // ---------------------------------------------------------------------------------
 // Float64 accumulation in channel order with prefetched windows (round 5) - the
 // reference-precision path (acc='f64': dedisperse, show=True, search_by_chunks).
 //
-// Same work decomposition as dedisp_kernel (8 waves x 8 trials x one 256-sample time tile,
-// lane l owning samples t0 + l + 64 k, k < 4), but:
+// Work decomposition: one DM tile of 64 consecutive trials x one 256-sample time tile per
+// workgroup of W waves x D trials (round 5 default W = 16, D = 4: 8 waves per SIMD), lane l
+// owning samples t0 + l + 64 k, k < 4.  Against round 4's dedisp_kernel (8 waves x 8 trials):
 //   * rows are float64 in LDS: float32 inputs are LDS-DMA'd raw and converted once per
 //     element and tile by the wave that DMA'd them (no conversion per window reload:
 //     the adds read the window registers directly); float64 inputs are DMA'd as they are.
@@ -26,16 +30,17 @@ namespace {
 //   * the window of a trial whose shift differs from the previous trial's is not read at
 //     that trial (a read + an immediate wait: the wave stalled on LDS latency at every
 //     reload, round 4) but PREFETCHED at the previous distinct window's turn: two window
-//     buffers w0 / w1, a state machine over the 8 trials (state S: wS current, the other
+//     buffers w0 / w1, a state machine over the D trials (state S: wS current, the other
 //     buffer in flight) whose code for each (trial, state) is written out, so a reload is
 //     wait + swap of roles with no register moves.  The last distinct window of a channel
 //     prefetches the next channel's first.
-// Record per (DM tile, channel, wave): 8 u32 words, word d: bit 31 trial d's window
-// differs from trial d - 1's (set for d = 0), bit 30 a window to prefetch when trial d's
-// becomes current, bits 17-29 trial d's window sample offset in its row (read for d = 0
-// at a chunk start), bits 0-16 the byte offset of the window to prefetch (from the
-// chunk's row base).  Channel order and the float64 adds are the reference's
-// (dedispersion.py:86-98): the series is bit-identical.
+// Record per (DM tile, channel, wave): D u32 words, word d: bit 31 trial d's window
+// differs from trial d - 1's (set for d = 0), bits 17-29 trial d's window sample offset
+// in its row (read for d = 0 at a chunk start), bits 0-16 the byte offset, from the
+// chunk's row base, of the window to prefetch when trial d's becomes current (0: none
+// left in the chunk - the prefetch then re-reads the row base, harmlessly).  Channel
+// order and the float64 adds are the reference's (dedispersion.py:86-98): the series is
+// bit-identical.
 
 // LDS-DMA of one float64 channel-row window [start, start + cover) mod n into dst
 __device__ __forceinline__ void dma_row_f64(unsigned char *dst, const double *row, int start, int cover_bytes, int n,
@@ -65,16 +70,27 @@ __device__ __forceinline__ void dma_row_f64(unsigned char *dst, const double *ro
     }
 }
 
-template <typename Tin, bool PLANE, bool STATS>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
+// Record of one (DM tile, channel, wave): D u32 words
+template <int D>
+struct F64Rec {
+    typedef uint32_t type __attribute__((ext_vector_type(D)));
+};
+
+// W waves x D trials per wave (W D = 64 trials per DM tile, kTPT).  W = 16, D = 4 (round 5
+// default): 1024-thread workgroups, two per CU, 8 waves per SIMD at <= 64 VGPRs - twice the
+// waves of W = 8, D = 8 to cover the window reads' latency.
+template <typename Tin, int W, int D, bool PLANE, bool STATS>
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W == 16 ? 8 : 4)))
 dedisp_f64_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const int32_t *__restrict__ tile_count,
                   const int32_t *__restrict__ tile_rowlen, const int32_t *__restrict__ base_tab,
-                  const u32x8 *__restrict__ rec_tab)
+                  const uint32_t *__restrict__ rec_tab)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr bool kConv = std::is_same<Tin, float>::value;  // raw float32 rows converted in LDS
     static_assert(kConv || std::is_same<Tin, double>::value, "dedisp_f64_kernel: float32 or float64 input");
-    constexpr int K = 4, TT = 64 * K, D = kD;
+    static_assert(W * D == kTPT && (D == 4 || D == 8), "dedisp_f64_kernel: W x D = 64 trials");
+    constexpr int K = 4, TT = 64 * K;
+    typedef typename F64Rec<D>::type rec_t;
 
     const int wg = pu::xcd_remap(blockIdx.x, gridDim.x);
     const int dt = a.dt0 + wg % a.ndt;
@@ -104,16 +120,16 @@ dedisp_f64_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const in
         for (int k = 0; k < K; ++k) acc[d][k] = 0.0;
 
     const int32_t *base = base_tab + (size_t)dt * a.nchan;
-    const u32x8 *recs = rec_tab + (size_t)dt * a.nchan * kWaves + wave;
+    const rec_t *recs = reinterpret_cast<const rec_t *>(rec_tab) + (size_t)dt * a.nchan * W + wave;
     const Tin *data = reinterpret_cast<const Tin *>(a.data);
     const int nchunks = (a.nchan + a.ncc - 1) / a.ncc;
 
-    // this wave's rows of chunk k: ci = wave + 8 m (it DMAs them and, for float32 inputs,
+    // this wave's rows of chunk k: ci = wave + W m (it DMAs them and, for float32 inputs,
     // converts them, so neither step needs a barrier of its own)
     auto issue_dma = [&](int k, int b) {
         const int c0 = k * a.ncc;
         const int nc = min(a.ncc, a.nchan - c0);
-        for (int ci = wave; ci < nc; ci += kWaves) {
+        for (int ci = wave; ci < nc; ci += W) {
             const int c = c0 + ci;
             int start = ld_uniform(base + c) + t0;
             if (start >= n) start -= n;
@@ -127,7 +143,7 @@ dedisp_f64_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const in
     };
     auto convert = [&](int k, int b) {
         const int nc = min(a.ncc, a.nchan - k * a.ncc);
-        for (int ci = wave; ci < nc; ci += kWaves) {
+        for (int ci = wave; ci < nc; ci += W) {
             const float *src = reinterpret_cast<const float *>(raw + ci * cover32);
             double *dst = reinterpret_cast<double *>(smem + b * buf_bytes + ci * chan_bytes);
             for (int j = 2 * lane; j < rowlen; j += 128) {
@@ -156,15 +172,16 @@ dedisp_f64_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const in
         }
         if (!active) continue;
         const uint32_t rows = smem_addr + (uint32_t)(b * buf_bytes) + 8u * lane;
-        const u32x8 *rc = recs + (size_t)c0 * kWaves;
-        u32x8 ra = ld_uniform(rc);
+        const rec_t *rc = recs + (size_t)c0 * W;
+        rec_t ra = ld_uniform(rc);
         double w0[4], w1[4];
         // chunk start: channel c0's first window into w1, state 0 (trial 0's reload makes
         // w1 current and prefetches the next window into w0)
         prefetch_window<4>(w1, rows + 8u * ((ra[0] >> 17) & 0x1fffu));
         // trial d in state S (P: label prefix, R: the channel's record): a reload waits for
-        // the other buffer, prefetches the next window into this one and continues in the
-        // other state.  Every (trial, state) has its own code: no register moves.
+        // the other buffer, prefetches the next window into this one (a harmless re-read of
+        // the row base when no window is left in the chunk) and continues in the other
+        // state.  Every (trial, state) has its own code: no register moves.
 #define PU_F64_ADD(D_, W_)                                                                      \
     {                                                                                          \
         acc[D_][0] += W_[0];                                                                   \
@@ -177,7 +194,7 @@ dedisp_f64_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const in
     P##T##D_##_##S_:                                                                           \
     if (R[D_] & 0x80000000u) {                                                                 \
         wait_window<4>(WO);                                                                    \
-        if (R[D_] & 0x40000000u) prefetch_window<4>(WS, rows + (R[D_] & 0x1ffffu));            \
+        prefetch_window<4>(WS, rows + (R[D_] & 0x1ffffu));                                     \
         PU_F64_ADD(D_, WO)                                                                     \
         goto P##T##D_##_flip_##S_;                                                             \
     }                                                                                          \
@@ -193,22 +210,24 @@ dedisp_f64_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const in
     goto P##T##N_##_1;                                                                         \
     P##T##D_##_flip_1:                                                                         \
     goto P##T##N_##_0;
-#define PU_F64_CHANNEL(P, R)                                                                   \
-    if (state) goto P##T0_1;                                                                   \
-    PU_F64_TRIAL(P, R, 0, 0, w0, w1) PU_F64_TRIAL(P, R, 0, 1, w1, w0) PU_F64_EDGES(P, 0, 1)    \
-    PU_F64_TRIAL(P, R, 1, 0, w0, w1) PU_F64_TRIAL(P, R, 1, 1, w1, w0) PU_F64_EDGES(P, 1, 2)    \
-    PU_F64_TRIAL(P, R, 2, 0, w0, w1) PU_F64_TRIAL(P, R, 2, 1, w1, w0) PU_F64_EDGES(P, 2, 3)    \
-    PU_F64_TRIAL(P, R, 3, 0, w0, w1) PU_F64_TRIAL(P, R, 3, 1, w1, w0) PU_F64_EDGES(P, 3, 4)    \
-    PU_F64_TRIAL(P, R, 4, 0, w0, w1) PU_F64_TRIAL(P, R, 4, 1, w1, w0) PU_F64_EDGES(P, 4, 5)    \
-    PU_F64_TRIAL(P, R, 5, 0, w0, w1) PU_F64_TRIAL(P, R, 5, 1, w1, w0) PU_F64_EDGES(P, 5, 6)    \
-    PU_F64_TRIAL(P, R, 6, 0, w0, w1) PU_F64_TRIAL(P, R, 6, 1, w1, w0) PU_F64_EDGES(P, 6, 7)    \
-    PU_F64_TRIAL(P, R, 7, 0, w0, w1) PU_F64_TRIAL(P, R, 7, 1, w1, w0) PU_F64_EDGES(P, 7, 8)    \
-    P##T8_0:                                                                                   \
+#define PU_F64_PAIR(P, R, D_, N_)                                                              \
+    PU_F64_TRIAL(P, R, D_, 0, w0, w1) PU_F64_TRIAL(P, R, D_, 1, w1, w0) PU_F64_EDGES(P, D_, N_)
+#define PU_F64_END(P, N_)                                                                      \
+    P##T##N_##_0:                                                                              \
     state = 0;                                                                                 \
     goto P##done;                                                                              \
-    P##T8_1:                                                                                   \
+    P##T##N_##_1:                                                                              \
     state = 1;                                                                                 \
     P##done:;
+#define PU_F64_CHANNEL4(P, R)                                                                  \
+    if (state) goto P##T0_1;                                                                   \
+    PU_F64_PAIR(P, R, 0, 1) PU_F64_PAIR(P, R, 1, 2) PU_F64_PAIR(P, R, 2, 3) PU_F64_PAIR(P, R, 3, 4) \
+    PU_F64_END(P, 4)
+#define PU_F64_CHANNEL8(P, R)                                                                  \
+    if (state) goto P##T0_1;                                                                   \
+    PU_F64_PAIR(P, R, 0, 1) PU_F64_PAIR(P, R, 1, 2) PU_F64_PAIR(P, R, 2, 3) PU_F64_PAIR(P, R, 3, 4) \
+    PU_F64_PAIR(P, R, 4, 5) PU_F64_PAIR(P, R, 5, 6) PU_F64_PAIR(P, R, 6, 7) PU_F64_PAIR(P, R, 7, 8) \
+    PU_F64_END(P, 8)
         // two channels per iteration with ping-pong records: a record is loaded a channel
         // ahead and consumed only after the channel before it (rotating one record through
         // a copy made the compiler wait for the just-issued scalar load at every channel
@@ -217,35 +236,49 @@ dedisp_f64_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const in
         int state = 0;
 #pragma nounroll
         for (int ci = 0; ci < nc; ci += 2) {
-            u32x8 rb = ld_uniform(rc + (size_t)min(ci + 1, nc - 1) * kWaves);
-            PU_F64_CHANNEL(A, ra)
+            rec_t rb = ld_uniform(rc + (size_t)min(ci + 1, nc - 1) * W);
+            if constexpr (D == 4) {
+                PU_F64_CHANNEL4(A4, ra)
+            } else {
+                PU_F64_CHANNEL8(A8, ra)
+            }
             asm volatile("" : "+s"(rb));
             if (ci + 1 >= nc) break;
-            ra = ld_uniform(rc + (size_t)min(ci + 2, nc - 1) * kWaves);
-            PU_F64_CHANNEL(B, rb)
+            ra = ld_uniform(rc + (size_t)min(ci + 2, nc - 1) * W);
+            if constexpr (D == 4) {
+                PU_F64_CHANNEL4(B4, rb)
+            } else {
+                PU_F64_CHANNEL8(B8, rb)
+            }
             asm volatile("" : "+s"(ra));
         }
 #undef PU_F64_ADD
 #undef PU_F64_TRIAL
 #undef PU_F64_EDGES
-#undef PU_F64_CHANNEL
+#undef PU_F64_PAIR
+#undef PU_F64_END
+#undef PU_F64_CHANNEL4
+#undef PU_F64_CHANNEL8
     }
     if (!active) return;
 
     if constexpr (STATS && !PLANE) {
         if (t0 + TT <= n) {
-            stats_full_f64<1, K>(acc, a, first, slot0, cnt, tt, lane);
+            stats_full_f64<1, K, D>(acc, a, first, slot0, cnt, tt, lane);
             return;
         }
     }
-    write_outputs<double, double, K, kD, PLANE, STATS>(acc, a, first, slot0, cnt, t0, tt, lane);
+    write_outputs<double, double, K, D, PLANE, STATS>(acc, a, first, slot0, cnt, t0, tt, lane);
 }
+
+// the production shape: 16 waves x 4 trials (kF64Waves in dedisperse.hip's planner)
+constexpr int kF64W = 16, kF64D = 4;
 
 template <typename Tin>
 int launch(bool plane, const DedispArgs &a, size_t lds_bytes, const int32_t *first, const int32_t *count,
-           const int32_t *rowlen, const int32_t *base, const u32x8 *rec8, hipStream_t s)
+           const int32_t *rowlen, const int32_t *base, const uint32_t *rec, hipStream_t s)
 {
-    const dim3 grid((unsigned)((int64_t)a.ndt * a.ntt_run)), block(kThreads);
+    const dim3 grid((unsigned)((int64_t)a.ndt * a.ntt_run)), block(64 * kF64W);
     auto go = [&](auto kern) {
         if (lds_bytes > 64 * 1024) {
             int rc = pu::hip_check(hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
@@ -253,10 +286,11 @@ int launch(bool plane, const DedispArgs &a, size_t lds_bytes, const int32_t *fir
                                    "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
             if (rc) return rc;
         }
-        hipLaunchKernelGGL(kern, grid, block, lds_bytes, s, a, first, count, rowlen, base, rec8);
+        hipLaunchKernelGGL(kern, grid, block, lds_bytes, s, a, first, count, rowlen, base, rec);
         return pu::launch_check("dedisp_f64_kernel");
     };
-    return plane ? go(dedisp_f64_kernel<Tin, true, false>) : go(dedisp_f64_kernel<Tin, false, true>);
+    return plane ? go(dedisp_f64_kernel<Tin, kF64W, kF64D, true, false>)
+                 : go(dedisp_f64_kernel<Tin, kF64W, kF64D, false, true>);
 }
 
 }  // namespace
@@ -264,11 +298,12 @@ int launch(bool plane, const DedispArgs &a, size_t lds_bytes, const int32_t *fir
 // Called by dedisperse.hip's dispatch (plain types across the translation units).
 int pu_dd_launch_f64(bool tin_f32, bool plane, const void *args, size_t args_bytes, size_t lds_bytes,
                      const int32_t *first, const int32_t *count, const int32_t *rowlen, const int32_t *base,
-                     const void *rec8, void *stream)
+                     const void *rec8, void *stream, int waves)
 {
+    PU_REQUIRE(waves == kF64W, "pu_dd_launch_f64: planned for %d waves, kernel built for %d", waves, kF64W);
     PU_REQUIRE(args_bytes == sizeof(DedispArgs), "pu_dd_launch_f64: argument block size mismatch");
     const DedispArgs &a = *reinterpret_cast<const DedispArgs *>(args);
-    const u32x8 *r = reinterpret_cast<const u32x8 *>(rec8);
+    const uint32_t *r = reinterpret_cast<const uint32_t *>(rec8);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     return tin_f32 ? launch<float>(plane, a, lds_bytes, first, count, rowlen, base, r, s)
                    : launch<double>(plane, a, lds_bytes, first, count, rowlen, base, r, s);

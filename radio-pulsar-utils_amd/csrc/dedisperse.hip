@@ -44,10 +44,12 @@
 
 #include "dedisp_common.h"
 
-// dedisp_f64.hip
+// dedisp_f64.hip (waves: the planner's kF64Waves, checked against the kernel's)
 int pu_dd_launch_f64(bool tin_f32, bool plane, const void *args, size_t args_bytes, size_t lds_bytes,
                      const int32_t *first, const int32_t *count, const int32_t *rowlen, const int32_t *base,
-                     const void *rec8, void *stream);
+                     const void *rec8, void *stream, int waves);
+// dedisp_f64_kernel's workgroup: 16 waves x 4 trials (= kTPT trials per DM tile)
+constexpr int kF64Waves = 16, kF64Trials = 4;
 
 namespace {
 
@@ -605,8 +607,12 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
         // chunk's two stores instead cost ~7 scalar issue slots per chunk on the CU's shared
         // scalar unit (C2 19.97 -> 19.20 ms, C3 625 trials 156.5 -> 150.9 ms).  When a copy
         // spans whole passes (copy_bytes a multiple of 256 UP: C2's 2560 B at UP = 10) the
-        // chunks past len only write the slot's own padding, so the stores need no guards.
-        const bool whole = copy_bytes % (256 * UP) == 0;
+        // chunks past len only write the slot's own padding, so the stores need no guards;
+        // so does any pass whose UP chunks end inside the copy (4 i0 + 256 UP <= copy_bytes:
+        // copy 1's stores end 4 bytes earlier than copy 0's) - round 5: C3's single pass per
+        // slot (272 elements, UP = 5) no longer guards each store by a scalar compare + branch
+        // when its copy is 6 chunks long.
+        const bool whole = copy_bytes % (256 * UP) == 0 || 4 * i0 + 256 * UP <= copy_bytes;
         asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(w0) : "memory");
         if (whole) {
 #pragma unroll
@@ -635,11 +641,16 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
     // slower: 22.1 / 25.6 vs 20.2 ms for halves / thirds - fewer reads in flight per
     // pass, and the extra pass code spilled registers.)
     auto build = [&](const i32x4 st, const meta_t m0) {
+        // the next slot's record is loaded a slot ahead (round 5: loaded on demand, its
+        // scalar-load latency stood in front of every slot after a wave's first)
+        meta_t m = m0;
         for (int s = st.z + wave; s < st.w; s += W) {
-            const meta_t m = s == st.z + wave ? m0 : ld_uniform(reinterpret_cast<const meta_t *>(slots + (size_t)s * MS));
+            const int sn = min(s + W, st.w - 1);
+            const meta_t mn = ld_uniform(reinterpret_cast<const meta_t *>(slots + (size_t)sn * MS));
             const int len = m[0], gs = m[3];
             const int lim = (len + 63) & ~63;
             for (int i0 = 0; i0 < len; i0 += 64 * U) build_pass(std::integral_constant<int, U>{}, m, gs, i0, lim);
+            m = mn;
         }
     };
 
@@ -982,7 +993,7 @@ struct pu_plan {
     size_t lds_bytes = 0;
     int32_t *d_first = nullptr, *d_count = nullptr, *d_rowlen = nullptr, *d_base = nullptr;
     u32x4 *d_rec = nullptr;
-    u32x8 *d_rec8 = nullptr;  // dedisp_f64_kernel's records
+    uint32_t *d_rec8 = nullptr;  // dedisp_f64_kernel's records (kF64Trials words per channel and wave)
     // subband mode (group > 1): per tile {first, count, raw row length, copy bytes},
     // stages {group begin, group end, item begin, item end}, build items, window records
     int group = 1, ngroups = 0, nslots_total = 0, raw_stride = 0, shape = SUB_WIDE;
@@ -1025,7 +1036,7 @@ int ensure_lds(Kern kern, size_t bytes)
 int launch_f64(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s, bool tin_f32)
 {
     return pu_dd_launch_f64(tin_f32, plane, &a, sizeof a, p->lds_bytes, p->d_first, p->d_count, p->d_rowlen,
-                            p->d_base, p->d_rec8, s);
+                            p->d_base, p->d_rec8, s, kF64Waves);
 }
 
 template <typename Tin, typename Tl, typename Ta>
@@ -1298,40 +1309,32 @@ int plan_channels(pu_plan *p, const int64_t *shifts, size_t budget)
     // next distinct window of the channel, else the next channel's first in the chunk)
     const size_t copy_bytes = (size_t)p->row_stride * esz;
     std::vector<u32x4> rec(fsm ? 0 : (size_t)ndt * nchan * kWaves);
-    std::vector<u32x8> rec8(fsm ? (size_t)ndt * nchan * kWaves : 0);
+    std::vector<uint32_t> rec8(fsm ? (size_t)ndt * nchan * kTPT : 0);  // kF64Waves x kF64Trials words
     if (fsm) {
         if (p->ncc * chan_bytes >= (int64_t(1) << 17) || max_spread >= (1 << 13)) {
             pu::set_error("pu_plan_create: float64 window records overflow");
             return PU_EUNSUPPORTED;
         }
+        constexpr int FD = kF64Trials;
         for (size_t t = 0; t < (size_t)ndt; ++t)
             for (int64_t c = 0; c < nchan; ++c)
-                for (int w = 0; w < kWaves; ++w) {
-                    const int32_t *rr = rel.data() + (t * nchan + c) * kTPT + w * kD;
+                for (int w = 0; w < kF64Waves; ++w) {
+                    const int32_t *rr = rel.data() + (t * nchan + c) * kTPT + w * FD;
                     const uint32_t cb = (uint32_t)((c % p->ncc) * chan_bytes);
                     // the window after the last distinct one of channel c: channel c + 1's
-                    // first, if it is in the same chunk
+                    // first, if it is in the same chunk (else 0: a harmless read of the row base)
                     const bool nxt_ok = c + 1 < nchan && (c + 1) % p->ncc != 0;
                     const uint32_t nxt_off =
-                        nxt_ok ? (uint32_t)(cb + chan_bytes + 8u * (uint32_t)rel[((t * nchan + c + 1) * kTPT) + w * kD])
+                        nxt_ok ? (uint32_t)(cb + chan_bytes + 8u * (uint32_t)rel[((t * nchan + c + 1) * kTPT) + w * FD])
                                : 0u;
-                    u32x8 r;
-                    for (int d = 0; d < kD; ++d) {
+                    uint32_t *r = rec8.data() + ((t * nchan + c) * kF64Waves + w) * FD;
+                    for (int d = 0; d < FD; ++d) {
                         const bool reload = d == 0 || rr[d] != rr[d - 1];
                         int e = d + 1;
-                        while (e < kD && rr[e] == rr[e - 1]) ++e;
-                        bool has = true;
-                        uint32_t off = 0;
-                        if (e < kD) {
-                            off = cb + 8u * (uint32_t)rr[e];
-                        } else {
-                            has = nxt_ok;
-                            off = nxt_off;
-                        }
-                        r[d] = (reload ? 0x80000000u : 0u) | (has && reload ? 0x40000000u : 0u) |
-                               ((uint32_t)rr[d] << 17) | (has && reload ? off : 0u);
+                        while (e < FD && rr[e] == rr[e - 1]) ++e;
+                        const uint32_t off = e < FD ? cb + 8u * (uint32_t)rr[e] : nxt_off;
+                        r[d] = (reload ? 0x80000000u : 0u) | ((uint32_t)rr[d] << 17) | (reload ? off : 0u);
                     }
-                    rec8[(t * nchan + c) * kWaves + w] = r;
                 }
     }
     for (size_t t = 0; t < (size_t)(fsm ? 0 : ndt); ++t)
@@ -1366,11 +1369,12 @@ int plan_channels(pu_plan *p, const int64_t *shifts, size_t budget)
             // staged rows (dedisp_f64_kernel on float32: + the raw row's DMA write and the
             // converting pass's read)
             lds_tile += nchan * (int64_t)E * p->row_stride * esz + (raw_bytes ? nchan * 2 * raw_bytes : 0);
-            for (int w = 0; w < kWaves && w * kD < count[t]; ++w)
+            const int WW = fsm ? kF64Waves : kWaves, DD = fsm ? kF64Trials : kD;
+            for (int w = 0; w < WW && w * DD < count[t]; ++w)
                 for (int64_t c = 0; c < nchan; ++c) {
-                    const int32_t *rr = rel.data() + (t * nchan + c) * kTPT + w * kD;
+                    const int32_t *rr = rel.data() + (t * nchan + c) * kTPT + w * DD;
                     int reads = 1;
-                    for (int d = 1; d < kD; ++d) reads += rr[d] != rr[d - 1] ? 1 : 0;
+                    for (int d = 1; d < DD; ++d) reads += rr[d] != rr[d - 1] ? 1 : 0;
                     lds_tile += (int64_t)reads * J * 64 * 8;
                 }
         }

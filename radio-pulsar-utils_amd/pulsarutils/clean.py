@@ -290,6 +290,32 @@ def _gaussian_weights_device(sigma, dev):
     return _WEIGHTS[key]
 
 
+_LC_WS = {}  # (device, workspace bytes) -> zero-filled workspace of pu_lc_factor (left zeroed by it)
+
+
+def light_curve_factor(lc, weights, radius, median_out=None):
+    """clean.py:79-80 on a device light curve: factor = np.median(lc_smooth) / lc_smooth with
+    lc_smooth = gaussian_filter(lc) (``weights``/``radius`` from _gaussian_weights_device),
+    bit for bit as pu_gaussian_filter1d + pu_median + pu_ratio_dev, in one launch
+    (pu_lc_factor).  ``median_out``: optional float64 device tensor [1] for the median."""
+    t = _hip.torch()
+    lib = _hip.lib()
+    n = lc.numel()
+    nbytes = lib.pu_lc_factor_workspace_bytes(n)
+    key = (str(lc.device), nbytes)
+    if key not in _LC_WS:
+        # zero-filled once: the kernel's barrier counters and first histogram buffer must be
+        # zero on entry, and it leaves them so
+        _LC_WS[key] = t.zeros(nbytes + 256, dtype=t.uint8, device=lc.device)
+    buf = _LC_WS[key]
+    off = (-buf.data_ptr()) % 256
+    factor = t.empty(n, dtype=t.float64, device=lc.device)
+    _hip.check(lib.pu_lc_factor(_hip.ptr(lc), n, _hip.ptr(weights), int(radius), _hip.ptr(factor),
+                                _hip.ptr(median_out) if median_out is not None else None, buf.data_ptr() + off,
+                                nbytes, _hip.stream_ptr()), "pu_lc_factor")
+    return factor
+
+
 def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=False, out=None,
                        zero_dm=False):
     """renormalize_data on a device tensor; returns (float64 device tensor, bad_bins or None),
@@ -297,8 +323,8 @@ def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=
     host: renormalize_data discards it, as the reference does).
 
     Passes (clean.py:73-105): zero-DM light curve over good channels (column means,
-    rows in order) -> gaussian_filter (GPU, scipy's order) -> median (GPU radix
-    select) -> factor
+    rows in order) -> gaussian_filter (scipy's order) + median (radix select) + factor in
+    one launch (pu_lc_factor)
     -> per-channel mean of x*factor (numpy pairwise order) -> (x*f - mu)/mu with bad
     channels zeroed [+ its column mean] -> uniform_filter1d(16) thresholds on the
     device (certified; scipy's own running sum on the device when a decision is
@@ -326,12 +352,8 @@ def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=
     lc = t.empty(n, dtype=t.float64, device=dev)
     _hip.check(lib.pu_col_means(_hip.ptr(x), code, nchan, n, x.stride(0), _hip.ptr(bad), _hip.ptr(lc), s),
                "pu_col_means")
-    smooth = t.empty(n, dtype=t.float64, device=dev)
-    _hip.check(lib.pu_gaussian_filter1d(_hip.ptr(lc), n, _hip.ptr(dw), radius, _hip.ptr(smooth), s),
-               "pu_gaussian_filter1d")
-    med = median_device(smooth)
-    factor = t.empty(n, dtype=t.float64, device=dev)
-    _hip.check(lib.pu_ratio_dev(_hip.ptr(med), _hip.ptr(smooth), n, _hip.ptr(factor), s), "pu_ratio_dev")
+    # gaussian_filter + np.median + the factor in one launch (pu_lc_factor)
+    factor = light_curve_factor(lc, dw, radius)
     spec = _row_sums(x, 2, scale=factor, divisor=n)
     if out is None:
         out = t.empty((nchan, n), dtype=t.float64, device=dev)

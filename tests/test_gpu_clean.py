@@ -491,3 +491,47 @@ def test_variability_one_pass_and_fallback(gpu):
         np.testing.assert_array_equal(got, want)
     finally:
         C.channel_variances_device = orig
+
+
+@pytest.mark.parametrize("n,sigma", [(262144, 101), (262145, 101), (262143, 55), (1, 1), (7, 2), (1000, 3),
+                                     (3 * 262144 + 17, 101), (2 * 262144, 0.2), (12345, 600)])
+def test_light_curve_factor_one_launch(gpu, n, sigma):
+    """pu_lc_factor (clean.py:79-80 in one launch with grid barriers: Gaussian, median,
+    factor) equals scipy's gaussian_filter1d + np.median + the division bit for bit, and the
+    launch-by-launch device path; several segments per workgroup (n > 2^18), odd and even
+    n, n < radius, a NaN (median NaN), a constant light curve, and r > 2048 (sigma 600: the
+    launch-by-launch fallback).  Repeated calls on the kept workspace (its counters must be
+    left reset) give the same bits."""
+    import torch
+    from scipy.ndimage import gaussian_filter1d
+    from pulsarutils import _hip
+    rng = np.random.default_rng(n)
+    dev = torch.device("cuda", 0)
+    dw, radius = C._gaussian_weights_device(sigma, dev)
+    cases = [rng.normal(size=n) * 10 + 100, np.full(n, 4.5)]
+    if n > 8:
+        spiky = rng.normal(size=n) + 50
+        spiky[rng.integers(0, n, 5)] = 1e6
+        cases.append(spiky)
+        nan = rng.normal(size=n) + 3
+        nan[n // 2] = np.nan
+        cases.append(nan)
+    lib = _hip.lib()
+    for x in cases:
+        smooth = gaussian_filter1d(x, sigma, mode="reflect")
+        med = np.median(smooth)
+        want = med / smooth
+        xd = torch.from_numpy(x).to(dev)
+        for rep in range(2):
+            medd = torch.empty(1, dtype=torch.float64, device=dev)
+            got = C.light_curve_factor(xd, dw, radius, median_out=medd)
+            np.testing.assert_array_equal(got.cpu().numpy(), want)
+            assert np.array_equal(medd.cpu().numpy(), [med], equal_nan=True)
+        # the launch-by-launch device path
+        sm = torch.empty_like(xd)
+        _hip.check(lib.pu_gaussian_filter1d(_hip.ptr(xd), n, _hip.ptr(dw), radius, _hip.ptr(sm), _hip.stream_ptr()),
+                   "pu_gaussian_filter1d")
+        f3 = torch.empty_like(xd)
+        _hip.check(lib.pu_ratio_dev(_hip.ptr(C.median_device(sm)), _hip.ptr(sm), n, _hip.ptr(f3), _hip.stream_ptr()),
+                   "pu_ratio_dev")
+        assert torch.equal(f3.isnan(), got.isnan()) and torch.equal(f3.nan_to_num(), got.nan_to_num())
