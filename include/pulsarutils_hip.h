@@ -257,10 +257,8 @@ int pu_ratio_dev(const double *numerator, const double *x, int64_t n, double *ou
 /* renormalize_data's light-curve chain (clean.py:77-82 after the zero-DM column means):
  * lc_smooth = gaussian_filter(lc, sigma) (weights: device [2r+1], as pu_gaussian_filter1d),
  * med = np.median(lc_smooth) (as pu_median), factor[t] = med / lc_smooth[t] (as
- * pu_ratio_dev) - the same bits as those three calls, in ONE launch with grid barriers when
- * r <= 2048 and n <= 2^21 on 256 CUs (otherwise the three).  median_out: device [1] or
- * NULL.  ws: pu_lc_factor_workspace_bytes(n), 256-byte aligned, zero-filled before its
- * first use (the kernel leaves it so for the next call). */
+ * pu_ratio_dev) - those three calls on one stream, with their scratch in one workspace.
+ * median_out: device [1] or NULL.  ws: pu_lc_factor_workspace_bytes(n), 256-byte aligned. */
 size_t pu_lc_factor_workspace_bytes(int64_t n);
 int pu_lc_factor(const double *lc, int64_t n, const double *weights, int64_t radius, double *factor,
                  double *median_out, void *ws, size_t ws_bytes, void *stream);

@@ -890,11 +890,9 @@ __device__ double reduce_sum_staged(const double *__restrict__ a, int64_t m, dou
 //  * bad = lc_rebin > 5 sd | lc_rebin < -3 sd (NaN compares false, as in numpy).
 // Restatement checked bit for bit against scipy / numpy on CPU
 // (tests/test_oracle.py::test_cut_outliers_exact_restatement).
-__global__ void __launch_bounds__(256)
-outlier_exact_kernel(const double *__restrict__ lc, int64_t n, OutlierState *st, double *__restrict__ v,
-                     double *__restrict__ tmp, uint8_t *__restrict__ mask, int32_t *__restrict__ list, int force)
+__device__ void outlier_exact_body(const double *__restrict__ lc, int64_t n, OutlierState *st, double *__restrict__ v,
+                                   double *__restrict__ tmp, uint8_t *__restrict__ mask, int32_t *__restrict__ list)
 {
-    if (!force && st->flag == 0) return;
     __shared__ double stage[kBlock];
     __shared__ double thr[2];
     constexpr int kSize = 16, kOrig = kSize / 2;  // window [i - 8, i + 7]
@@ -951,6 +949,14 @@ outlier_exact_kernel(const double *__restrict__ lc, int64_t n, OutlierState *st,
         mask[i] = b;
         if (b) list[atomicAdd(&st->nbad, 1u)] = (int32_t)i;  // any order: the zeroing is idempotent
     }
+}
+
+__global__ void __launch_bounds__(256)
+outlier_exact_kernel(const double *__restrict__ lc, int64_t n, OutlierState *st, double *__restrict__ v,
+                     double *__restrict__ tmp, uint8_t *__restrict__ mask, int32_t *__restrict__ list, int force)
+{
+    if (!force && st->flag == 0) return;
+    outlier_exact_body(lc, n, st, v, tmp, mask, list);
 }
 
 // Zero the plane's bad columns (the final list): one workgroup per row, the list's
@@ -1144,31 +1150,17 @@ __global__ void __launch_bounds__(256) median_final_kernel(MedState *st, const u
     }
 }
 
-// ---------------------------------------------------------------- light-curve factor
-// renormalize_data's 2^18-point chain in ONE launch (round 5; clean.py:77-82):
-//   lc_smooth = gaussian_filter(lc, sigma)      scipy's order (gauss_quad_segment)
-//   med = np.median(lc_smooth)                  the radix select above, six digit passes
-//   factor = med / lc_smooth                    as ratio_dev_kernel
-// Until round 4 these were 10 launches (Gaussian, median init + 6 histogram passes + final,
-// ratio).  Here each workgroup computes the Gaussian of its 1024-sample segments into LDS
-// and keeps them there; the select's digit passes histogram those LDS values and are
-// separated by grid barriers (a monotonic arrival counter: every histogram-adding wave's
-// vmcnt(0), the workgroup barrier, lane 0's agent release, the arrival, a relaxed poll with
-// s_sleep, the agent acquire - MI355X_MICROARCH.md, inter-workgroup visibility) instead of
-// kernel boundaries; the factor is written from the LDS values at the end.  Co-residency:
-// the grid is at most one workgroup per CU and a workgroup takes <= ~110 KB of LDS at the
-// largest supported n, so every workgroup of the grid is resident at once on the whole
-// device (the cleaning kernels never run on a CU-masked stream).
-// The histogram buffers rotate as in pu_median: pass p clears buffer (p + 1) % 3, whose last
-// reader was pass p - 1's select (before barrier p - 1); pass 5 clears buffer 0, so the
-// workspace leaves as it must enter (buffer 0 zero); the last workgroup out resets the
-// counters.
-constexpr int kLcThreads = 256;
-constexpr int kLcSeg = 4 * kLcThreads;  // Gaussian outputs per segment
-constexpr int kLcMaxSegs = 8;           // segments per workgroup kept in LDS (64 KB)
-
+// ---------------------------------------------------------------- grid barrier
+// A monotonic arrival counter for the one-launch cut_outliers (every wave's vmcnt(0), the
+// workgroup barrier, lane 0's agent release, the arrival, a relaxed poll with s_sleep, the
+// agent acquire - MI355X_MICROARCH.md, inter-workgroup visibility).  Round 5 also tried it
+// for renormalize_data's light-curve chain (Gaussian + six radix-select passes + ratio in one
+// launch, smoothed values kept in LDS): 103 us with this barrier, 123 us with the fenced form
+// of every pass, against 79 us for the ten launches (scripts/bench_lc.py, n = 2^18, sigma
+// 101): at 256 workgroups a barrier costs ~7 us, a kernel boundary ~1.5 us, so the chain
+// stays launch-by-launch (pu_lc_factor).
 struct LcState {
-    unsigned arrive;  // grid-barrier arrivals within a launch
+    unsigned arrive;  // grid-barrier arrivals within a launch (outlier_fused_kernel)
     unsigned leave;   // workgroups past the last barrier
     unsigned nan;     // NaNs among the smoothed values
     unsigned pad[61];
@@ -1191,120 +1183,165 @@ __device__ __forceinline__ void lc_grid_barrier(LcState *st, unsigned target)
     __syncthreads();
 }
 
-__global__ void __launch_bounds__(kLcThreads)
-lc_factor_kernel(const double *__restrict__ lc, int64_t n, const double *__restrict__ w, int r, int segs,
-                 double *__restrict__ factor, double *__restrict__ med_out, LcState *st, uint32_t *hist)
+// ---------------------------------------------------------------- cut_outliers, one launch
+// pu_cut_outliers' window means, std, certified decisions, exact fallback and column zeroing
+// (clean.py:93-105) in ONE launch (round 5; until round 4: a state fill + five kernels).
+// Phases separated by grid barriers (lc_grid_barrier; the counters sit in the workspace
+// head cleared by the call's one 128-byte fill):
+//   1. each workgroup: u = the 16-window means of its segments (kept in LDS and stored for
+//      the exact path), the partial sum of u[::16], max |lc| and the NaN flag;
+//   2. mean of u[::16] -> the partial sum of squared deviations;
+//   3. sd, thresholds and certification margins (every workgroup computes the same values
+//      from the same totals) -> the mask, the ambiguity flag, the bad-bin list;
+//   4. only when the flag is set: workgroup 0 redoes the mask with the reference's own
+//      arithmetic (outlier_exact_body), the others wait;
+//   5. the bad columns of the plane zeroed, rows dealt over the workgroups.
+// The sums in phases 1-2 are float64 atomics (any order: the certification margins bound
+// the difference from scipy's chain, as in outlier_std_kernel).
+struct OutlierBar {
+    unsigned arrive, leave;
+    double sum_u16, sum_sq;
+};
+
+__global__ void __launch_bounds__(256)
+outlier_fused_kernel(const double *__restrict__ lc, int64_t n, OutlierState *st, OutlierBar *ob,
+                     double *__restrict__ u, double *__restrict__ u16, uint8_t *__restrict__ mask,
+                     int32_t *__restrict__ list, double *__restrict__ out, int64_t nrows, int64_t ld_out, int segs)
 {
-    extern __shared__ __attribute__((aligned(16))) double lsm[];
-    const int gwords = ((r + 2) & ~1) + kLcSeg + 2 * r + 2 * kGaussPad;
-    double *vals = lsm;                                                  // [segs][kLcSeg]
-    double *gsm = lsm + segs * kLcSeg;                                   // Gaussian staging
-    uint32_t *h = reinterpret_cast<uint32_t *>(gsm + gwords);            // [2][kMedBins]
-    uint32_t *scan = h + 2 * kMedBins;                                   // [256]
-    int64_t *res = reinterpret_cast<int64_t *>(scan + kLcThreads);       // [2]
+    extern __shared__ __attribute__((aligned(16))) double usm[];  // [segs][1024] window means
+    __shared__ double red[4];
+    __shared__ unsigned long long wm[4];
     const int t = threadIdx.x;
     const unsigned G = gridDim.x;
-    // 1. the smoothed values of segments blockIdx.x + G s
-    uint32_t nans = 0;
+    LcState *bar = reinterpret_cast<LcState *>(ob);  // arrive at offset 0 (lc_grid_barrier's counter)
+    auto block_sum = [&](double v) {
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        __syncthreads();
+        if ((t & 63) == 0) red[t >> 6] = v;
+        __syncthreads();
+        return (red[0] + red[1]) + (red[2] + red[3]);
+    };
+    // 1. window means, sum of u[::16], max |lc|, NaN
+    double s16 = 0.0;
+    unsigned long long lb = 0;
+    bool nan = false;
     for (int sg = 0; sg < segs; ++sg) {
-        const int64_t i0 = ((int64_t)blockIdx.x + (int64_t)G * sg) * kLcSeg;
-        if (i0 >= n) break;  // uniform
-        double a[4];
-        gauss_quad_segment<kLcThreads>(lc, n, w, r, i0, gsm, a);
-        const int64_t i = i0 + 4 * t;
+        const int64_t i0 = ((int64_t)blockIdx.x + (int64_t)G * sg) * 1024;
+        if (i0 >= n) break;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            vals[sg * kLcSeg + 4 * t + q] = a[q];
-            nans += (i + q < n && a[q] != a[q]) ? 1u : 0u;
-        }
-        __syncthreads();  // every thread is done with the staging before it is refilled
-    }
-    if (nans) atomicAdd(&st->nan, nans);
-    // 2. radix select of ranks k0 = n/2 - 1 (n even; n/2 odd) and k1 = n/2
-    uint64_t pfx[2] = {0, 0};
-    int64_t kk[2] = {(n % 2 == 0) ? n / 2 - 1 : n / 2, n / 2};
-    for (int pass = 0; pass < kMedPasses; ++pass) {
-        if (pass > 0) {
-            const uint32_t *hp = hist + (size_t)((pass - 1) % kMedBufs) * 2 * kMedBins;
-            for (int j = 0; j < 2; ++j) {
-                int bin;
-                int64_t rem;
-                med_select_block(hp + j * kMedBins, kk[j], scan, res, bin, rem);
-                pfx[j] |= (uint64_t)bin << med_shift(pass - 1);
-                kk[j] = rem;
+            const int64_t i = i0 + q * 256 + t;
+            double w = 0.0;
+            if (i < n) {
+                double sw = 0.0;
+                for (int j = -8; j < 8; ++j) sw += lc[(i + j >= 0 && i + j < n) ? i + j : reflect_small(i + j, n)];
+                w = sw / 16.0;
+                u[i] = w;
+                if ((i & 15) == 0) {
+                    u16[i >> 4] = w;
+                    s16 += w;
+                }
+                const double x = lc[i];
+                nan = nan || x != x;
+                const unsigned long long ab = (unsigned long long)__double_as_longlong(fabs(x));
+                lb = ab > lb ? ab : lb;
             }
+            usm[sg * 1024 + q * 256 + t] = w;
         }
-        uint32_t *nxt = hist + (size_t)((pass + 1) % kMedBufs) * 2 * kMedBins;
-        for (int i = blockIdx.x * kLcThreads + t; i < 2 * kMedBins; i += G * kLcThreads) nxt[i] = 0;
-        for (int i = t; i < 2 * kMedBins; i += kLcThreads) h[i] = 0;
-        __syncthreads();
-        const int shift = med_shift(pass), bits = med_bits(pass);
-        const uint64_t dmask = (uint64_t(1) << bits) - 1;
-        const int hs = shift + bits;  // bits above the digit must match the prefix
-        for (int sg = 0; sg < segs; ++sg) {
-            const int64_t i0 = ((int64_t)blockIdx.x + (int64_t)G * sg) * kLcSeg;
-            if (i0 >= n) break;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const double d = vals[sg * kLcSeg + 4 * t + q];
-                if (i0 + 4 * t + q >= n || d != d) continue;
-                const uint64_t k = order_key(d);
-                const uint32_t dig = (uint32_t)((k >> shift) & dmask);
-                if (hs >= 64 || (k >> hs) == (pfx[0] >> hs)) atomicAdd(&h[dig], 1u);
-                if (hs >= 64 || (k >> hs) == (pfx[1] >> hs)) atomicAdd(&h[kMedBins + dig], 1u);
-            }
-        }
-        __syncthreads();
-        uint32_t *cur = hist + (size_t)(pass % kMedBufs) * 2 * kMedBins;
-        for (int i = t; i < 2 * kMedBins; i += kLcThreads) {
-            const uint32_t c = h[i];
-            if (c) atomicAdd(&cur[i], c);
-        }
-        lc_grid_barrier(st, G * (unsigned)(pass + 1));
     }
-    // 3. the last digit, numpy's mean of the two order statistics (NaN if any NaN), factor
     {
-        const uint32_t *hp = hist + (size_t)((kMedPasses - 1) % kMedBufs) * 2 * kMedBins;
-        for (int j = 0; j < 2; ++j) {
-            int bin;
-            int64_t rem;
-            med_select_block(hp + j * kMedBins, kk[j], scan, res, bin, rem);
-            pfx[j] |= (uint64_t)bin << med_shift(kMedPasses - 1);
+        const double tot = block_sum(s16);
+        unsigned long long b = nan ? ~0ull : lb;
+        for (int off = 32; off > 0; off >>= 1) {
+            const unsigned long long o = __shfl_xor(b, off, 64);
+            b = o > b ? o : b;
+        }
+        if ((t & 63) == 0) wm[t >> 6] = b;
+        __syncthreads();
+        if (t == 0) {
+            unsigned long long m = wm[0];
+            for (int w = 1; w < 4; ++w) m = wm[w] > m ? wm[w] : m;
+            if (m == ~0ull) atomicOr(&st->flag, 1u);
+            else atomicMax(&st->lbits, m);
+            atomicAdd(&ob->sum_u16, tot);
         }
     }
-    const bool any_nan = __hip_atomic_load(&st->nan, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-    double med;
-    if (any_nan) {
-        med = __longlong_as_double(0x7ff8000000000000ll);
-    } else {
-        const double a = key_value(pfx[0]);
-        med = (n % 2 == 0) ? (0.0 + ((0.0 + a) + key_value(pfx[1]))) / 2.0 : (0.0 + (0.0 + a)) / 1.0;
-    }
-    if (blockIdx.x == 0 && t == 0 && med_out) med_out[0] = med;
+    lc_grid_barrier(bar, G);
+    // 2. squared deviations of u[::16] from their mean
+    const int64_t m = (n + 15) / 16;
+    const double mean = __hip_atomic_load(&ob->sum_u16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) / (double)m;
+    double ssq = 0.0;
     for (int sg = 0; sg < segs; ++sg) {
-        const int64_t i0 = ((int64_t)blockIdx.x + (int64_t)G * sg) * kLcSeg;
+        const int64_t i0 = ((int64_t)blockIdx.x + (int64_t)G * sg) * 1024;
         if (i0 >= n) break;
-        const int64_t i = i0 + 4 * t;
-        if (i + 3 < n && (reinterpret_cast<uintptr_t>(factor) & 15) == 0) {
-            const double *v = vals + sg * kLcSeg + 4 * t;
-            *reinterpret_cast<f64x2 *>(factor + i) = f64x2{med / v[0], med / v[1]};
-            *reinterpret_cast<f64x2 *>(factor + i + 2) = f64x2{med / v[2], med / v[3]};
-        } else {
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (i + q < n) factor[i + q] = med / vals[sg * kLcSeg + 4 * t + q];
+        for (int q = 0; q < 4; ++q) {
+            const int64_t i = i0 + q * 256 + t;
+            if (i < n && (i & 15) == 0) {
+                const double d = usm[sg * 1024 + q * 256 + t] - mean;
+                ssq += d * d;
+            }
         }
     }
-    // 4. the last workgroup out resets the counters (every workgroup has passed every
-    // barrier and read the NaN count)
-    __syncthreads();
-    if (t == 0) {
-        const unsigned before = __hip_atomic_fetch_add(&st->leave, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (before == G - 1) {
-            __hip_atomic_store(&st->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&st->nan, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&st->leave, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    {
+        const double tot = block_sum(ssq);
+        if (t == 0) atomicAdd(&ob->sum_sq, tot);
+    }
+    lc_grid_barrier(bar, 2 * G);
+    // 3. thresholds, margins (outlier_std_kernel's), decisions, the bad-bin list
+    const double ss = __hip_atomic_load(&ob->sum_sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const double sd = sqrt(ss / (double)m);
+    const double L = __longlong_as_double(
+        (long long)__hip_atomic_load(&st->lbits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const double E = ((double)(2 * n + 64) * 0x1p-53) * L + 1e-300;
+    const double Es = E + 1e-12 * sd;
+    const double up = 5.0 * sd, down = -3.0 * sd;
+    const double margin_up = E + 5.0 * Es + 1e-15 * (L + 5.0 * sd);
+    const double margin_down = E + 3.0 * Es + 1e-15 * (L + 3.0 * sd);
+    if (blockIdx.x == 0 && t == 0) {
+        st->sd = sd;
+        st->up = up;
+        st->down = down;
+        st->margin_up = margin_up;
+        st->margin_down = margin_down;
+        if (sd != sd) atomicOr(&st->flag, 1u);
+    }
+    const int lane = t & 63;
+    for (int sg = 0; sg < segs; ++sg) {
+        const int64_t i0 = ((int64_t)blockIdx.x + (int64_t)G * sg) * 1024;
+        if (i0 >= n) break;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t i = i0 + q * 256 + t;
+            uint8_t b = 0;
+            if (i < n) {
+                const double v = usm[sg * 1024 + q * 256 + t];
+                const double du = v - up, dd = v - down;
+                const bool amb = !(fabs(du) > margin_up) || !(fabs(dd) > margin_down);
+                if (amb) atomicOr(&st->flag, 1u);
+                b = (du > 0.0 || dd < 0.0) ? 1 : 0;
+                mask[i] = b;
+            }
+            const uint64_t bal = __ballot(b != 0);
+            if (bal) {
+                uint32_t base = 0;
+                if (lane == __ffsll((unsigned long long)bal) - 1) base = atomicAdd(&st->nbad, (uint32_t)__popcll(bal));
+                base = __shfl(base, __ffsll((unsigned long long)bal) - 1, 64);
+                if (b) list[base + __popcll(bal & ((uint64_t(1) << lane) - 1))] = (int32_t)i;
+            }
         }
+    }
+    lc_grid_barrier(bar, 3 * G);
+    // 4. the rare exact path (uniform: every workgroup reads the same flag)
+    if (__hip_atomic_load(&st->flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+        if (blockIdx.x == 0) outlier_exact_body(lc, n, st, u, u16, mask, list);
+        lc_grid_barrier(bar, 4 * G);
+    }
+    // 5. zero the bad columns, rows over the workgroups
+    const uint32_t nbad = __hip_atomic_load(&st->nbad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int64_t r = blockIdx.x; r < nrows; r += G) {
+        double *row = out + r * ld_out;
+        for (uint32_t k = t; k < nbad; k += 256) row[list[k]] = 0.0;
     }
 }
 
@@ -1796,6 +1833,29 @@ int cut_outliers(const double *lc, int64_t n, double *out, int64_t nrows, int64_
     PU_REQUIRE(nrows < (int64_t(1) << 31), "pu_cut_outliers: too many rows");
     // one 16-byte-multiple fill (the runtime splits a 56-byte memset into two kernels)
     static_assert(sizeof(OutlierState) <= 64, "OutlierState fits the cleared 64 bytes");
+    static_assert(sizeof(OutlierBar) <= 64, "OutlierBar fits the cleared 64 bytes after the state");
+    if (!exact_only) {
+        // one launch with grid barriers (outlier_fused_kernel): at most one workgroup per two
+        // CUs, each with <= 64 KB of window means in LDS, so the whole grid is resident
+        static int cus = 0;
+        if (!cus) PU_TRY_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+        const int64_t nseg = (n + 1023) / 1024;
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(nseg, std::max(1, cus / 2)));
+        const int segs = (int)((nseg + grid - 1) / grid);
+        if (segs <= 8 && nrows < (int64_t(1) << 31)) {
+            static bool attr_set = false;  // 64 KB static (the exact path's staging) + the window means
+            if (!attr_set) {
+                PU_TRY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(outlier_fused_kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 8 * 1024 * (int)sizeof(double)));
+                attr_set = true;
+            }
+            PU_TRY_HIP(hipMemsetAsync(st, 0, 128, s));
+            OutlierBar *ob = reinterpret_cast<OutlierBar *>(reinterpret_cast<char *>(ws) + 64);
+            hipLaunchKernelGGL(outlier_fused_kernel, dim3(grid), dim3(256), (size_t)segs * 1024 * sizeof(double), s, lc,
+                               n, st, ob, u, u16, mask, list, out, nrows, ld_out, segs);
+            return pu::launch_check("outlier_fused_kernel");
+        }
+    }
     PU_TRY_HIP(hipMemsetAsync(st, 0, 64, s));
     if (!exact_only) {
         hipLaunchKernelGGL(outlier_window_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, lc, n, u, u16, st);
@@ -1867,40 +1927,10 @@ int pu_ratio_dev(const double *numerator, const double *x, int64_t n, double *ou
     return pu::launch_check("ratio_dev_kernel");
 }
 
-namespace {
-struct LcGeom {
-    bool fused;
-    int grid, segs;
-    size_t lds;
-};
-
-LcGeom lc_geom(int64_t n, int64_t r)
-{
-    LcGeom g{false, 0, 0, 0};
-    static int cus[64] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return g;
-    if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return g;
-    if (r > kGaussMaxR || n <= 0 || cus[dev] <= 0) return g;
-    const int64_t nseg = (n + kLcSeg - 1) / kLcSeg;
-    g.grid = (int)std::min<int64_t>(nseg, cus[dev]);
-    g.segs = (int)((nseg + g.grid - 1) / g.grid);
-    const int64_t gwords = ((r + 2) & ~int64_t(1)) + kLcSeg + 2 * r + 2 * kGaussPad;
-    g.lds = (size_t)g.segs * kLcSeg * 8 + (size_t)gwords * 8 + 2 * kMedBins * 4 + kLcThreads * 4 + 16;
-    g.fused = g.segs <= kLcMaxSegs && g.lds <= 160 * 1024;
-    return g;
-}
-
-size_t lc_head_bytes() { return sizeof(LcState) + (size_t)kMedBufs * 2 * kMedBins * sizeof(uint32_t); }
-}  // namespace
-
 size_t pu_lc_factor_workspace_bytes(int64_t n)
 {
-    // fused: the state and the three histogram buffers; otherwise (r > kGaussMaxR or a very
-    // long series) also the smoothed series, pu_median's workspace and the median
-    const size_t head = lc_head_bytes();
-    return head + (((size_t)std::max<int64_t>(n, 0) * 8 + 255) & ~size_t(255)) + pu_median_workspace_bytes() + 64;
+    // the smoothed series, pu_median's workspace and the median
+    return (((size_t)std::max<int64_t>(n, 0) * 8 + 255) & ~size_t(255)) + pu_median_workspace_bytes() + 64;
 }
 
 int pu_lc_factor(const double *lc, int64_t n, const double *w, int64_t r, double *factor, double *median_out, void *ws,
@@ -1909,25 +1939,11 @@ int pu_lc_factor(const double *lc, int64_t n, const double *w, int64_t r, double
     PU_REQUIRE(lc && w && factor && n > 0 && r >= 0, "pu_lc_factor: bad arguments");
     PU_REQUIRE(ws && ws_bytes >= pu_lc_factor_workspace_bytes(n) && reinterpret_cast<uintptr_t>(ws) % 256 == 0,
                "pu_lc_factor: workspace too small or not 256-byte aligned");
-    hipStream_t s = pu::as_stream(stream);
     char *wsb = reinterpret_cast<char *>(ws);
-    const LcGeom g = lc_geom(n, r);
-    if (g.fused) {
-        static bool attr_set = false;
-        if (!attr_set) {
-            PU_TRY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(lc_factor_kernel),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-            attr_set = true;
-        }
-        LcState *st = reinterpret_cast<LcState *>(wsb);
-        uint32_t *hist = reinterpret_cast<uint32_t *>(st + 1);
-        hipLaunchKernelGGL(lc_factor_kernel, dim3(g.grid), dim3(kLcThreads), g.lds, s, lc, n, w, (int)r, g.segs, factor,
-                           median_out, st, hist);
-        return pu::launch_check("lc_factor_kernel");
-    }
-    // the launch-by-launch path: Gaussian, median, ratio
-    double *smooth = reinterpret_cast<double *>(wsb + lc_head_bytes());
-    char *mws = wsb + lc_head_bytes() + (((size_t)n * 8 + 255) & ~size_t(255));
+    // Gaussian, median, ratio, launch by launch (a one-launch form with grid barriers measured
+    // slower: see the grid-barrier note above)
+    double *smooth = reinterpret_cast<double *>(wsb);
+    char *mws = wsb + (((size_t)n * 8 + 255) & ~size_t(255));
     double *med = reinterpret_cast<double *>(mws + pu_median_workspace_bytes());
     int rc = pu_gaussian_filter1d(lc, n, w, r, smooth, stream);
     if (!rc) rc = pu_median(smooth, n, median_out ? median_out : med, mws, pu_median_workspace_bytes(), stream);

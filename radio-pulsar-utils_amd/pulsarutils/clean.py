@@ -290,28 +290,21 @@ def _gaussian_weights_device(sigma, dev):
     return _WEIGHTS[key]
 
 
-_LC_WS = {}  # (device, workspace bytes) -> zero-filled workspace of pu_lc_factor (left zeroed by it)
-
-
 def light_curve_factor(lc, weights, radius, median_out=None):
     """clean.py:79-80 on a device light curve: factor = np.median(lc_smooth) / lc_smooth with
     lc_smooth = gaussian_filter(lc) (``weights``/``radius`` from _gaussian_weights_device),
-    bit for bit as pu_gaussian_filter1d + pu_median + pu_ratio_dev, in one launch
-    (pu_lc_factor).  ``median_out``: optional float64 device tensor [1] for the median."""
+    bit for bit as pu_gaussian_filter1d + pu_median + pu_ratio_dev (pu_lc_factor: those
+    three on the current stream).  ``median_out``: optional float64 device tensor [1]."""
     t = _hip.torch()
     lib = _hip.lib()
     n = lc.numel()
     nbytes = lib.pu_lc_factor_workspace_bytes(n)
-    key = (str(lc.device), nbytes)
-    if key not in _LC_WS:
-        # zero-filled once: the kernel's barrier counters and first histogram buffer must be
-        # zero on entry, and it leaves them so
-        _LC_WS[key] = t.zeros(nbytes + 256, dtype=t.uint8, device=lc.device)
-    buf = _LC_WS[key]
-    off = (-buf.data_ptr()) % 256
+    # the caching allocator's blocks are stream-ordered and 512-byte aligned
+    buf = t.empty(nbytes, dtype=t.uint8, device=lc.device)
+    assert buf.data_ptr() % 256 == 0
     factor = t.empty(n, dtype=t.float64, device=lc.device)
     _hip.check(lib.pu_lc_factor(_hip.ptr(lc), n, _hip.ptr(weights), int(radius), _hip.ptr(factor),
-                                _hip.ptr(median_out) if median_out is not None else None, buf.data_ptr() + off,
+                                _hip.ptr(median_out) if median_out is not None else None, buf.data_ptr(),
                                 nbytes, _hip.stream_ptr()), "pu_lc_factor")
     return factor
 
@@ -324,7 +317,7 @@ def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=
 
     Passes (clean.py:73-105): zero-DM light curve over good channels (column means,
     rows in order) -> gaussian_filter (scipy's order) + median (radix select) + factor in
-    one launch (pu_lc_factor)
+    pu_lc_factor
     -> per-channel mean of x*factor (numpy pairwise order) -> (x*f - mu)/mu with bad
     channels zeroed [+ its column mean] -> uniform_filter1d(16) thresholds on the
     device (certified; scipy's own running sum on the device when a decision is
@@ -352,7 +345,7 @@ def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=
     lc = t.empty(n, dtype=t.float64, device=dev)
     _hip.check(lib.pu_col_means(_hip.ptr(x), code, nchan, n, x.stride(0), _hip.ptr(bad), _hip.ptr(lc), s),
                "pu_col_means")
-    # gaussian_filter + np.median + the factor in one launch (pu_lc_factor)
+    # gaussian_filter + np.median + the factor (pu_lc_factor)
     factor = light_curve_factor(lc, dw, radius)
     spec = _row_sums(x, 2, scale=factor, divisor=n)
     if out is None:

@@ -54,6 +54,20 @@ def test_m0_consumers_checked_on_device_code():
     assert " 0 reading" in r.stdout, r.stdout
 
 
+def test_every_launch_stub_has_a_device_image():
+    """A host object with a stale embedded code object links but aborts at launch ("Cannot
+    find Symbol"): every launch stub in the shipped library has its kernel descriptor."""
+    import subprocess
+    import sys
+    lib = os.path.join(REPO, "radio-pulsar-utils_amd", "pulsarutils", "_lib", "libpulsarutils_hip.so")
+    if not os.path.exists(lib):
+        pytest.skip("library not built here")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "scripts", "check_stubs.py"), lib],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert " 0 without a device image" in r.stdout, r.stdout
+
+
 def test_plan_opts_validated_without_gpu():
     """pu_plan_create_ex checks its options before any HIP call."""
     from pulsarutils import _hip

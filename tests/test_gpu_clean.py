@@ -495,13 +495,11 @@ def test_variability_one_pass_and_fallback(gpu):
 
 @pytest.mark.parametrize("n,sigma", [(262144, 101), (262145, 101), (262143, 55), (1, 1), (7, 2), (1000, 3),
                                      (3 * 262144 + 17, 101), (2 * 262144, 0.2), (12345, 600)])
-def test_light_curve_factor_one_launch(gpu, n, sigma):
-    """pu_lc_factor (clean.py:79-80 in one launch with grid barriers: Gaussian, median,
-    factor) equals scipy's gaussian_filter1d + np.median + the division bit for bit, and the
-    launch-by-launch device path; several segments per workgroup (n > 2^18), odd and even
-    n, n < radius, a NaN (median NaN), a constant light curve, and r > 2048 (sigma 600: the
-    launch-by-launch fallback).  Repeated calls on the kept workspace (its counters must be
-    left reset) give the same bits."""
+def test_light_curve_factor(gpu, n, sigma):
+    """pu_lc_factor (clean.py:79-80: Gaussian, median, factor) equals scipy's
+    gaussian_filter1d + np.median + the division bit for bit, and the three separate device
+    calls; long series (n > 2^18), odd and even n, n < radius, a NaN (median NaN), a
+    constant light curve, r > 2048 (sigma 600).  Repeated calls give the same bits."""
     import torch
     from scipy.ndimage import gaussian_filter1d
     from pulsarutils import _hip
