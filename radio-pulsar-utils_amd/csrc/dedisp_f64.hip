@@ -34,13 +34,21 @@ namespace {
 //     buffer in flight) whose code for each (trial, state) is written out, so a reload is
 //     wait + swap of roles with no register moves.  The last distinct window of a channel
 //     prefetches the next channel's first.
-// Record per (DM tile, channel, wave): D u32 words, word d: bit 31 trial d's window
-// differs from trial d - 1's (set for d = 0), bits 17-29 trial d's window sample offset
-// in its row (read for d = 0 at a chunk start), bits 0-16 the byte offset, from the
-// chunk's row base, of the window to prefetch when trial d's becomes current (0: none
-// left in the chunk - the prefetch then re-reads the row base, harmlessly).  Channel
-// order and the float64 adds are the reference's (dedispersion.py:86-98): the series is
-// bit-identical.
+//   * no scalar memory traffic in the channel loop: the window records travel with the
+//     rows (one 256-byte LDS-DMA per channel and chunk, all waves' records), each channel's
+//     record is read from LDS one channel ahead and moved into scalars after the wait that
+//     trial 0 needs anyway; every channel's reload count is even (planner), so channels
+//     start and end in state 0 and no state variable crosses them.  Per channel: four
+//     v_readfirstlane, D - 1 scalar compares and the loop's two (round 5's first form,
+//     scalar-loaded records two channels per iteration with a state carried over: ~22
+//     scalar instructions per channel, more than its vector ones - SQ_INSTS_SALU 1.26x
+//     SQ_INSTS_VALU at C2, profiles/r05/counters/).
+// Record per (DM tile, channel, wave): D u32 words, word d = 0 when trial d reads trial
+// d - 1's window, else 1 + the byte offset, from the chunk's row base, of the window to
+// prefetch when trial d's becomes current (planner: dedisperse.hip, pu_plan create).  A
+// table after the records holds each channel's first window offset (read at chunk starts).
+// Channel order and the float64 adds are the reference's (dedispersion.py:86-98): the
+// series is bit-identical.
 
 // LDS-DMA of one float64 channel-row window [start, start + cover) mod n into dst
 __device__ __forceinline__ void dma_row_f64(unsigned char *dst, const double *row, int start, int cover_bytes, int n,
@@ -70,27 +78,41 @@ __device__ __forceinline__ void dma_row_f64(unsigned char *dst, const double *ro
     }
 }
 
-// Record of one (DM tile, channel, wave): D u32 words
-template <int D>
-struct F64Rec {
-    typedef uint32_t type __attribute__((ext_vector_type(D)));
-};
+// One channel's record (D = 4 u32, uniform across the wave) read from LDS into VGPRs,
+// issued without a wait; wait_window_record() waits for it together with a window.
+__device__ __forceinline__ void prefetch_record(u32x4 &r, uint32_t addr)
+{
+    asm volatile("ds_read_b128 %0, %1" : "=&v"(r) : "v"(addr) : "memory");
+}
+__device__ __forceinline__ void wait_window_record(double (&w)[4], u32x4 &r)
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(r) : : "memory");
+}
+__device__ __forceinline__ u32x4 readfirstlane4(const u32x4 &v)
+{
+    u32x4 s;
+    s[0] = __builtin_amdgcn_readfirstlane(v[0]);
+    s[1] = __builtin_amdgcn_readfirstlane(v[1]);
+    s[2] = __builtin_amdgcn_readfirstlane(v[2]);
+    s[3] = __builtin_amdgcn_readfirstlane(v[3]);
+    return s;
+}
 
-// W waves x D trials per wave (W D = 64 trials per DM tile, kTPT).  W = 16, D = 4 (round 5
-// default): 1024-thread workgroups, two per CU, 8 waves per SIMD at <= 64 VGPRs - twice the
-// waves of W = 8, D = 8 to cover the window reads' latency.
+// W waves x D trials per wave (W D = 64 trials per DM tile, kTPT): W = 16, D = 4 -
+// 1024-thread workgroups, two per CU, 8 waves per SIMD at <= 64 VGPRs to cover the window
+// reads' latency (round 5: against W = 8, D = 8 at 4 waves per SIMD, 72.2 -> 66.4 ms at C2).
 template <typename Tin, int W, int D, bool PLANE, bool STATS>
-__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W == 16 ? 8 : 4)))
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(8)))
 dedisp_f64_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const int32_t *__restrict__ tile_count,
                   const int32_t *__restrict__ tile_rowlen, const int32_t *__restrict__ base_tab,
-                  const uint32_t *__restrict__ rec_tab)
+                  const uint32_t *__restrict__ rec_tab, const uint32_t *__restrict__ first_tab)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr bool kConv = std::is_same<Tin, float>::value;  // raw float32 rows converted in LDS
     static_assert(kConv || std::is_same<Tin, double>::value, "dedisp_f64_kernel: float32 or float64 input");
-    static_assert(W * D == kTPT && (D == 4 || D == 8), "dedisp_f64_kernel: W x D = 64 trials");
+    static_assert(W * D == kTPT && D == 4 && W == 16, "dedisp_f64_kernel: 16 waves x 4 trials");
     constexpr int K = 4, TT = 64 * K;
-    typedef typename F64Rec<D>::type rec_t;
+    constexpr int kRecBytes = 4 * D * W;  // one channel's records, all waves: one DMA instruction
 
     const int wg = pu::xcd_remap(blockIdx.x, gridDim.x);
     const int dt = a.dt0 + wg % a.ndt;
@@ -110,7 +132,10 @@ dedisp_f64_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const in
     const int buf_bytes = a.ncc * chan_bytes;
     const int cover64 = (rowlen * 8 + 255) & ~255;  // bytes of a float64 row moved by DMA
     const int cover32 = (rowlen * 4 + 255) & ~255;  // bytes of a raw float32 row (its stride too)
+    const int raw_bytes = kConv ? a.ncc * ((a.row_stride * 4 + 255) & ~255) : 0;
+    const int rec_slot = (a.ncc + 2) * kRecBytes;   // + 2 channels: the pipeline's read-ahead
     unsigned char *raw = smem + 2 * buf_bytes;
+    unsigned char *recs_lds = smem + 2 * buf_bytes + raw_bytes;
     const uint32_t smem_addr = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char *)smem;
 
     double acc[D][K];
@@ -120,12 +145,14 @@ dedisp_f64_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const in
         for (int k = 0; k < K; ++k) acc[d][k] = 0.0;
 
     const int32_t *base = base_tab + (size_t)dt * a.nchan;
-    const rec_t *recs = reinterpret_cast<const rec_t *>(rec_tab) + (size_t)dt * a.nchan * W + wave;
+    const uint32_t *rec_g = rec_tab + (size_t)dt * a.nchan * (D * W);
+    const uint32_t *first_g = first_tab + (size_t)dt * a.nchan * W + wave;
     const Tin *data = reinterpret_cast<const Tin *>(a.data);
     const int nchunks = (a.nchan + a.ncc - 1) / a.ncc;
 
-    // this wave's rows of chunk k: ci = wave + W m (it DMAs them and, for float32 inputs,
-    // converts them, so neither step needs a barrier of its own)
+    // this wave's rows of chunk k, ci = wave + W m, and their channels' records (it DMAs
+    // them and, for float32 inputs, converts the rows, so neither step needs a barrier of
+    // its own); rows into float64 buffer b (float64 input) or the raw buffer (float32)
     auto issue_dma = [&](int k, int b) {
         const int c0 = k * a.ncc;
         const int nc = min(a.ncc, a.nchan - c0);
@@ -139,6 +166,15 @@ dedisp_f64_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const in
                 dma_row_f32(raw + ci * cover32, row, start, cover32, n, small_n, lane);
             else
                 dma_row_f64(smem + b * buf_bytes + ci * chan_bytes, row, start, cover64, n, small_n, lane);
+            // the lane's byte offset made opaque here: hoisted out of the chunk loop, the
+            // per-lane 64-bit address (rec_g + lane) stayed live across the sum and spilled
+            uint32_t lane4 = 4u * (uint32_t)lane;
+            asm volatile("" : "+v"(lane4));
+            __builtin_amdgcn_global_load_lds((const void *)(reinterpret_cast<const char *>(rec_g + (size_t)c * (D * W)) +
+                                                            lane4),
+                                             (__attribute__((address_space(3))) void *)(recs_lds + (k & 1) * rec_slot +
+                                                                                         ci * kRecBytes),
+                                             4, 0, 0);
         }
     };
     auto convert = [&](int k, int b) {
@@ -164,7 +200,7 @@ dedisp_f64_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const in
             // buffer b was last read in chunk k - 2's sum, before every wave's barrier of
             // chunk k - 1
             convert(k, b);
-            __syncthreads();  // buffer b complete
+            __syncthreads();  // buffer b and record slot b complete
             if (k + 1 < nchunks) issue_dma(k + 1, 0);  // this wave's raw rows are converted
         } else {
             __syncthreads();  // buffer b landed; every wave left buffer b ^ 1
@@ -172,16 +208,24 @@ dedisp_f64_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const in
         }
         if (!active) continue;
         const uint32_t rows = smem_addr + (uint32_t)(b * buf_bytes) + 8u * lane;
-        const rec_t *rc = recs + (size_t)c0 * W;
-        rec_t ra = ld_uniform(rc);
+        const uint32_t rows_m1 = rows - 1u;  // reload words are 1 + the byte offset
+        // this wave's records of the chunk in LDS: channel ci at rec_v + ci * kRecBytes
+        uint32_t rec_v = smem_addr + (uint32_t)(2 * buf_bytes + raw_bytes + b * rec_slot + wave * 4 * D);
         double w0[4], w1[4];
-        // chunk start: channel c0's first window into w1, state 0 (trial 0's reload makes
-        // w1 current and prefetches the next window into w0)
-        prefetch_window<4>(w1, rows + 8u * ((ra[0] >> 17) & 0x1fffu));
-        // trial d in state S (P: label prefix, R: the channel's record): a reload waits for
-        // the other buffer, prefetches the next window into this one (a harmless re-read of
-        // the row base when no window is left in the chunk) and continues in the other
-        // state.  Every (trial, state) has its own code: no register moves.
+        u32x4 vr;
+        // chunk start: channel c0's first window into w1 (state 0: trial 0 makes w1
+        // current) and its record in flight
+        prefetch_window<4>(w1, rows + ld_uniform(first_g + (size_t)c0 * W));
+        prefetch_record(vr, rec_v);
+        // Channel code: trial 0 always reloads (w1 -> current, the next window prefetched
+        // into w0); trials 1..D-1 run a two-state machine (state S: wS current, the other
+        // buffer in flight) whose code for each (trial, state) is written out, so a reload is
+        // a wait + a swap of roles with no register moves.  The planner makes every channel's
+        // reload count even (a trial re-reading its predecessor's window where needed), so a
+        // channel always ends in state 0 with the next channel's first window in flight in
+        // w1: the code has one entry and one exit, and no state crosses channels.  Trial 0's
+        // wait also covers the channel's record (read during the previous channel's trial 0),
+        // which it moves into scalars before starting the next channel's read.
 #define PU_F64_ADD(D_, W_)                                                                      \
     {                                                                                          \
         acc[D_][0] += W_[0];                                                                   \
@@ -192,15 +236,14 @@ dedisp_f64_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const in
     }
 #define PU_F64_TRIAL(P, R, D_, S_, WS, WO)                                                     \
     P##T##D_##_##S_:                                                                           \
-    if (R[D_] & 0x80000000u) {                                                                 \
+    if (R[D_] != 0u) {                                                                         \
         wait_window<4>(WO);                                                                    \
-        prefetch_window<4>(WS, rows + (R[D_] & 0x1ffffu));                                     \
+        prefetch_window<4>(WS, rows_m1 + R[D_]);                                               \
         PU_F64_ADD(D_, WO)                                                                     \
         goto P##T##D_##_flip_##S_;                                                             \
     }                                                                                          \
     PU_F64_ADD(D_, WS)                                                                         \
     goto P##T##D_##_keep_##S_;
-        // every label's successor: (d + 1, same state) or (d + 1, other state)
 #define PU_F64_EDGES(P, D_, N_)                                                                \
     P##T##D_##_keep_0:                                                                         \
     goto P##T##N_##_0;                                                                         \
@@ -210,55 +253,32 @@ dedisp_f64_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const in
     goto P##T##N_##_1;                                                                         \
     P##T##D_##_flip_1:                                                                         \
     goto P##T##N_##_0;
-#define PU_F64_PAIR(P, R, D_, N_)                                                              \
-    PU_F64_TRIAL(P, R, D_, 0, w0, w1) PU_F64_TRIAL(P, R, D_, 1, w1, w0) PU_F64_EDGES(P, D_, N_)
-#define PU_F64_END(P, N_)                                                                      \
-    P##T##N_##_0:                                                                              \
-    state = 0;                                                                                 \
-    goto P##done;                                                                              \
-    P##T##N_##_1:                                                                              \
-    state = 1;                                                                                 \
-    P##done:;
-#define PU_F64_CHANNEL4(P, R)                                                                  \
-    if (state) goto P##T0_1;                                                                   \
-    PU_F64_PAIR(P, R, 0, 1) PU_F64_PAIR(P, R, 1, 2) PU_F64_PAIR(P, R, 2, 3) PU_F64_PAIR(P, R, 3, 4) \
-    PU_F64_END(P, 4)
-#define PU_F64_CHANNEL8(P, R)                                                                  \
-    if (state) goto P##T0_1;                                                                   \
-    PU_F64_PAIR(P, R, 0, 1) PU_F64_PAIR(P, R, 1, 2) PU_F64_PAIR(P, R, 2, 3) PU_F64_PAIR(P, R, 3, 4) \
-    PU_F64_PAIR(P, R, 4, 5) PU_F64_PAIR(P, R, 5, 6) PU_F64_PAIR(P, R, 6, 7) PU_F64_PAIR(P, R, 7, 8) \
-    PU_F64_END(P, 8)
-        // two channels per iteration with ping-pong records: a record is loaded a channel
-        // ahead and consumed only after the channel before it (rotating one record through
-        // a copy made the compiler wait for the just-issued scalar load at every channel
-        // start); a real loop, not unrolled (LLVM unrolled round 5's first goto cycle ~20
-        // times and spilled); the state carries over in a scalar
-        int state = 0;
+#define PU_F64_CHANNEL(P, R, RO)                                                               \
+    wait_window_record(w1, vr);                                                                \
+    const u32x4 R = readfirstlane4(vr);                                                        \
+    prefetch_record(vr, RO);                                                                   \
+    prefetch_window<4>(w0, rows_m1 + R[0]);                                                    \
+    PU_F64_ADD(0, w1)                                                                          \
+    goto P##T1_1;                                                                              \
+    PU_F64_TRIAL(P, R, 1, 0, w0, w1) PU_F64_TRIAL(P, R, 1, 1, w1, w0) PU_F64_EDGES(P, 1, 2)    \
+    PU_F64_TRIAL(P, R, 2, 0, w0, w1) PU_F64_TRIAL(P, R, 2, 1, w1, w0) PU_F64_EDGES(P, 2, 3)    \
+    PU_F64_TRIAL(P, R, 3, 0, w0, w1) PU_F64_TRIAL(P, R, 3, 1, w1, w0) PU_F64_EDGES(P, 3, 4)    \
+    P##T4_1: /* never reached (even reload counts); joins state 0 without a special exit */    \
+    goto P##T4_0;                                                                              \
+    P##T4_0:;
+        // a real loop, not unrolled (LLVM unrolled round 5's first goto cycle ~20 times and
+        // spilled)
 #pragma nounroll
-        for (int ci = 0; ci < nc; ci += 2) {
-            rec_t rb = ld_uniform(rc + (size_t)min(ci + 1, nc - 1) * W);
-            if constexpr (D == 4) {
-                PU_F64_CHANNEL4(A4, ra)
-            } else {
-                PU_F64_CHANNEL8(A8, ra)
-            }
-            asm volatile("" : "+s"(rb));
-            if (ci + 1 >= nc) break;
-            ra = ld_uniform(rc + (size_t)min(ci + 2, nc - 1) * W);
-            if constexpr (D == 4) {
-                PU_F64_CHANNEL4(B4, rb)
-            } else {
-                PU_F64_CHANNEL8(B8, rb)
-            }
-            asm volatile("" : "+s"(ra));
+        for (int ci = 0; ci < nc; ++ci) {
+            PU_F64_CHANNEL(A, rec, rec_v + (ci + 1) * kRecBytes)
         }
+        // the last prefetches (a re-read of the row base, or a record past the chunk's)
+        // land before the next chunk's DMA can overwrite anything
+        wait_window_record(w1, vr);
 #undef PU_F64_ADD
 #undef PU_F64_TRIAL
 #undef PU_F64_EDGES
-#undef PU_F64_PAIR
-#undef PU_F64_END
-#undef PU_F64_CHANNEL4
-#undef PU_F64_CHANNEL8
+#undef PU_F64_CHANNEL
     }
     if (!active) return;
 
@@ -276,7 +296,7 @@ constexpr int kF64W = 16, kF64D = 4;
 
 template <typename Tin>
 int launch(bool plane, const DedispArgs &a, size_t lds_bytes, const int32_t *first, const int32_t *count,
-           const int32_t *rowlen, const int32_t *base, const uint32_t *rec, hipStream_t s)
+           const int32_t *rowlen, const int32_t *base, const uint32_t *rec, const uint32_t *first_off, hipStream_t s)
 {
     const dim3 grid((unsigned)((int64_t)a.ndt * a.ntt_run)), block(64 * kF64W);
     auto go = [&](auto kern) {
@@ -286,7 +306,7 @@ int launch(bool plane, const DedispArgs &a, size_t lds_bytes, const int32_t *fir
                                    "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
             if (rc) return rc;
         }
-        hipLaunchKernelGGL(kern, grid, block, lds_bytes, s, a, first, count, rowlen, base, rec);
+        hipLaunchKernelGGL(kern, grid, block, lds_bytes, s, a, first, count, rowlen, base, rec, first_off);
         return pu::launch_check("dedisp_f64_kernel");
     };
     return plane ? go(dedisp_f64_kernel<Tin, kF64W, kF64D, true, false>)
@@ -298,13 +318,14 @@ int launch(bool plane, const DedispArgs &a, size_t lds_bytes, const int32_t *fir
 // Called by dedisperse.hip's dispatch (plain types across the translation units).
 int pu_dd_launch_f64(bool tin_f32, bool plane, const void *args, size_t args_bytes, size_t lds_bytes,
                      const int32_t *first, const int32_t *count, const int32_t *rowlen, const int32_t *base,
-                     const void *rec8, void *stream, int waves)
+                     const void *rec8, const void *first_off, void *stream, int waves)
 {
     PU_REQUIRE(waves == kF64W, "pu_dd_launch_f64: planned for %d waves, kernel built for %d", waves, kF64W);
     PU_REQUIRE(args_bytes == sizeof(DedispArgs), "pu_dd_launch_f64: argument block size mismatch");
     const DedispArgs &a = *reinterpret_cast<const DedispArgs *>(args);
     const uint32_t *r = reinterpret_cast<const uint32_t *>(rec8);
+    const uint32_t *f = reinterpret_cast<const uint32_t *>(first_off);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    return tin_f32 ? launch<float>(plane, a, lds_bytes, first, count, rowlen, base, r, s)
-                   : launch<double>(plane, a, lds_bytes, first, count, rowlen, base, r, s);
+    return tin_f32 ? launch<float>(plane, a, lds_bytes, first, count, rowlen, base, r, f, s)
+                   : launch<double>(plane, a, lds_bytes, first, count, rowlen, base, r, f, s);
 }

@@ -47,7 +47,7 @@
 // dedisp_f64.hip (waves: the planner's kF64Waves, checked against the kernel's)
 int pu_dd_launch_f64(bool tin_f32, bool plane, const void *args, size_t args_bytes, size_t lds_bytes,
                      const int32_t *first, const int32_t *count, const int32_t *rowlen, const int32_t *base,
-                     const void *rec8, void *stream, int waves);
+                     const void *rec8, const void *first_off, void *stream, int waves);
 // dedisp_f64_kernel's workgroup: 16 waves x 4 trials (= kTPT trials per DM tile)
 constexpr int kF64Waves = 16, kF64Trials = 4;
 
@@ -1035,8 +1035,10 @@ int ensure_lds(Kern kern, size_t bytes)
 // dedisp_f64_kernel (dedisp_f64.hip, its own translation unit and code-generation options)
 int launch_f64(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s, bool tin_f32)
 {
+    // records, then the first-window table (planner: one upload)
+    const uint32_t *first_off = p->d_rec8 + (size_t)p->ndt * p->nchan * kTPT;
     return pu_dd_launch_f64(tin_f32, plane, &a, sizeof a, p->lds_bytes, p->d_first, p->d_count, p->d_rowlen,
-                            p->d_base, p->d_rec8, s, kF64Waves);
+                            p->d_base, p->d_rec8, first_off, s, kF64Waves);
 }
 
 template <typename Tin, typename Tl, typename Ta>
@@ -1293,47 +1295,69 @@ int plan_channels(pu_plan *p, const int64_t *shifts, size_t budget)
     p->max_spread = max_spread;
     // dedisp_f64_kernel: two float64 row buffers, plus one raw float32 row per channel for
     // float32 inputs (whole 256-byte DMA pieces)
-    const int64_t raw_bytes = fsm && p->dtype == PU_F32 ? ((int64_t)max_rowlen * 4 + 255) / 256 * 256 : 0;
-    const int64_t per_chan = nbuf * chan_bytes + raw_bytes;
-    p->ncc = (int)std::max<int64_t>(1, std::min<int64_t>(nchan, (int64_t)(budget / per_chan)));
-    p->lds_bytes = (size_t)p->ncc * per_chan;
+    // (its stride: the row_stride's, as the kernel computes it), and two slots of window
+    // records (one 256-byte DMA per channel, + 2 channels of read-ahead each)
+    const int64_t raw_bytes = fsm && p->dtype == PU_F32 ? ((int64_t)p->row_stride * 4 + 255) / 256 * 256 : 0;
+    constexpr int64_t kRecChan = 4 * kTPT;
+    const int64_t per_chan = nbuf * chan_bytes + raw_bytes + (fsm ? 2 * kRecChan : 0);
+    const int64_t fixed = fsm ? 2 * 2 * kRecChan : 0;
+    p->ncc = (int)std::max<int64_t>(1, std::min<int64_t>(nchan, (int64_t)((budget - fixed) / per_chan)));
+    p->lds_bytes = (size_t)p->ncc * per_chan + fixed;
     if (p->lds_bytes > 160 * 1024) {
         pu::set_error("pu_plan_create: LDS row of %d elements does not fit", p->row_stride);
         return PU_EUNSUPPORTED;
     }
     // window records: per (tile, channel, wave) 8 x u16 = LDS byte offset of each
     // trial's window inside the row slot | (differs from the previous trial) << 15
-    // (dedisp_kernel), or 8 x u32 (dedisp_f64_kernel: word d = reload flag << 31 |
-    // prefetch flag << 30 | trial d's sample offset in its row << 17 | the byte offset, from
-    // the chunk's row base, of the window to prefetch when trial d's becomes current: the
-    // next distinct window of the channel, else the next channel's first in the chunk)
+    // (dedisp_kernel); dedisp_f64_kernel: kF64Trials u32 per (tile, channel, wave), word d =
+    // 0 if trial d reads the window of trial d - 1, else 1 + the byte offset, from the
+    // chunk's row base, of the window to PREFETCH when trial d's becomes current (the next
+    // reloading trial's, after the channel's last reload the next channel's first, 0 + 1
+    // past the chunk: a harmless read of the row base); every channel's reload count is
+    // made even (trial 0 always reloads; an odd count gets the last non-reloading trial
+    // reloaded too, re-reading its predecessor's window) so that each channel starts and
+    // ends in the kernel's state 0.  After the records: per (tile, channel, wave) the byte
+    // offset of the channel's first window (read at chunk starts).
     const size_t copy_bytes = (size_t)p->row_stride * esz;
     std::vector<u32x4> rec(fsm ? 0 : (size_t)ndt * nchan * kWaves);
-    std::vector<uint32_t> rec8(fsm ? (size_t)ndt * nchan * kTPT : 0);  // kF64Waves x kF64Trials words
+    std::vector<uint32_t> rec8(fsm ? (size_t)ndt * nchan * kTPT + (size_t)ndt * nchan * kF64Waves : 0);
+    int64_t f64_reads = 0;  // window reads of dedisp_f64_kernel, per launch and time tile
     if (fsm) {
-        if (p->ncc * chan_bytes >= (int64_t(1) << 17) || max_spread >= (1 << 13)) {
+        if (p->ncc * chan_bytes + 1 >= (int64_t(1) << 31)) {
             pu::set_error("pu_plan_create: float64 window records overflow");
             return PU_EUNSUPPORTED;
         }
         constexpr int FD = kF64Trials;
+        uint32_t *first8 = rec8.data() + (size_t)ndt * nchan * kTPT;
         for (size_t t = 0; t < (size_t)ndt; ++t)
             for (int64_t c = 0; c < nchan; ++c)
                 for (int w = 0; w < kF64Waves; ++w) {
                     const int32_t *rr = rel.data() + (t * nchan + c) * kTPT + w * FD;
                     const uint32_t cb = (uint32_t)((c % p->ncc) * chan_bytes);
-                    // the window after the last distinct one of channel c: channel c + 1's
-                    // first, if it is in the same chunk (else 0: a harmless read of the row base)
+                    first8[(t * nchan + c) * kF64Waves + w] = cb + 8u * (uint32_t)rr[0];
                     const bool nxt_ok = c + 1 < nchan && (c + 1) % p->ncc != 0;
                     const uint32_t nxt_off =
                         nxt_ok ? (uint32_t)(cb + chan_bytes + 8u * (uint32_t)rel[((t * nchan + c + 1) * kTPT) + w * FD])
                                : 0u;
+                    bool reload[FD];
+                    int nre = 0;
+                    for (int d = 0; d < FD; ++d) {
+                        reload[d] = d == 0 || rr[d] != rr[d - 1];
+                        nre += reload[d];
+                    }
+                    if (nre & 1)
+                        for (int d = FD - 1; d > 0; --d)
+                            if (!reload[d]) {
+                                reload[d] = true;
+                                break;
+                            }
                     uint32_t *r = rec8.data() + ((t * nchan + c) * kF64Waves + w) * FD;
                     for (int d = 0; d < FD; ++d) {
-                        const bool reload = d == 0 || rr[d] != rr[d - 1];
                         int e = d + 1;
-                        while (e < FD && rr[e] == rr[e - 1]) ++e;
+                        while (e < FD && !reload[e]) ++e;
                         const uint32_t off = e < FD ? cb + 8u * (uint32_t)rr[e] : nxt_off;
-                        r[d] = (reload ? 0x80000000u : 0u) | ((uint32_t)rr[d] << 17) | (reload ? off : 0u);
+                        r[d] = reload[d] ? off + 1u : 0u;
+                        if (reload[d] && w * FD < count[t]) f64_reads += 1;
                     }
                 }
     }
@@ -1369,15 +1393,16 @@ int plan_channels(pu_plan *p, const int64_t *shifts, size_t budget)
             // staged rows (dedisp_f64_kernel on float32: + the raw row's DMA write and the
             // converting pass's read)
             lds_tile += nchan * (int64_t)E * p->row_stride * esz + (raw_bytes ? nchan * 2 * raw_bytes : 0);
-            const int WW = fsm ? kF64Waves : kWaves, DD = fsm ? kF64Trials : kD;
-            for (int w = 0; w < WW && w * DD < count[t]; ++w)
+            if (fsm) continue;  // the float64 kernel's reads: f64_reads (records, below)
+            for (int w = 0; w < kWaves && w * kD < count[t]; ++w)
                 for (int64_t c = 0; c < nchan; ++c) {
-                    const int32_t *rr = rel.data() + (t * nchan + c) * kTPT + w * DD;
+                    const int32_t *rr = rel.data() + (t * nchan + c) * kTPT + w * kD;
                     int reads = 1;
-                    for (int d = 1; d < DD; ++d) reads += rr[d] != rr[d - 1] ? 1 : 0;
+                    for (int d = 1; d < kD; ++d) reads += rr[d] != rr[d - 1] ? 1 : 0;
                     lds_tile += (int64_t)reads * J * 64 * 8;
                 }
         }
+        lds_tile += f64_reads * J * 64 * 8;
         p->lds_traffic = lds_tile * p->ntt;
     }
     p->tile_first = first;
