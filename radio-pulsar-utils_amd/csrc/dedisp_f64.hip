@@ -37,15 +37,15 @@ namespace {
 //   * no scalar memory traffic in the channel loop: the window records travel with the
 //     rows (one 256-byte LDS-DMA per channel and chunk, all waves' records), each channel's
 //     record is read from LDS one channel ahead and moved into scalars after the wait that
-//     trial 0 needs anyway; every channel's reload count is even (planner), so channels
-//     start and end in state 0 and no state variable crosses them.  Per channel: four
-//     v_readfirstlane, D - 1 scalar compares and the loop's two (round 5's first form,
+//     trial 0 needs anyway; every channel pair's reload count is even (planner), so pairs
+//     start and end in state 0 and no state variable crosses them.  Per channel: two
+//     v_readfirstlane, D - 1 scalar tests and the loop's two (round 5's first form,
 //     scalar-loaded records two channels per iteration with a state carried over: ~22
 //     scalar instructions per channel, more than its vector ones - SQ_INSTS_SALU 1.26x
 //     SQ_INSTS_VALU at C2, profiles/r05/counters/).
-// Record per (DM tile, channel, wave): D u32 words, word d = 0 when trial d reads trial
-// d - 1's window, else 1 + the byte offset, from the chunk's row base, of the window to
-// prefetch when trial d's becomes current (planner: dedisperse.hip, pu_plan create).  A
+// Record per (DM tile, channel, wave): D u16 words, word d = 0 when trial d reads trial
+// d - 1's window, else 1 + the offset in float64 elements, from the chunk's row base, of
+// the window to prefetch when trial d's becomes current (planner: dedisperse.hip, pu_plan create).  A
 // table after the records holds each channel's first window offset (read at chunk starts).
 // Channel order and the float64 adds are the reference's (dedispersion.py:86-98): the
 // series is bit-identical.
@@ -78,25 +78,28 @@ __device__ __forceinline__ void dma_row_f64(unsigned char *dst, const double *ro
     }
 }
 
-// One channel's record (D = 4 u32, uniform across the wave) read from LDS into VGPRs,
-// issued without a wait; wait_window_record() waits for it together with a window.
-__device__ __forceinline__ void prefetch_record(u32x4 &r, uint32_t addr)
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// One channel's record (D = 4 u16, uniform across the wave) read from LDS into VGPRs,
+// issued without a wait (ds_read_b64: 2 LDS cycles, a 16-byte record's ds_read_b128 takes
+// 4); wait_window_record() waits for it together with a window.
+__device__ __forceinline__ void prefetch_record(u32x2 &r, uint32_t addr)
 {
-    asm volatile("ds_read_b128 %0, %1" : "=&v"(r) : "v"(addr) : "memory");
+    asm volatile("ds_read_b64 %0, %1" : "=&v"(r) : "v"(addr) : "memory");
 }
-__device__ __forceinline__ void wait_window_record(double (&w)[4], u32x4 &r)
+__device__ __forceinline__ void wait_window_record(double (&w)[4], u32x2 &r)
 {
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(r) : : "memory");
 }
-__device__ __forceinline__ u32x4 readfirstlane4(const u32x4 &v)
+__device__ __forceinline__ u32x2 readfirstlane2(const u32x2 &v)
 {
-    u32x4 s;
+    u32x2 s;
     s[0] = __builtin_amdgcn_readfirstlane(v[0]);
     s[1] = __builtin_amdgcn_readfirstlane(v[1]);
-    s[2] = __builtin_amdgcn_readfirstlane(v[2]);
-    s[3] = __builtin_amdgcn_readfirstlane(v[3]);
     return s;
 }
+// word d of a record in scalars (d0 | d1 << 16, d2 | d3 << 16)
+#define PU_F64_WORD(R, D_) (((D_) & 1) ? (R[(D_) >> 1] >> 16) : (R[(D_) >> 1] & 0xffffu))
 
 // W waves x D trials per wave (W D = 64 trials per DM tile, kTPT): W = 16, D = 4 -
 // 1024-thread workgroups, two per CU, 8 waves per SIMD at <= 64 VGPRs to cover the window
@@ -112,7 +115,7 @@ dedisp_f64_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const in
     static_assert(kConv || std::is_same<Tin, double>::value, "dedisp_f64_kernel: float32 or float64 input");
     static_assert(W * D == kTPT && D == 4 && W == 16, "dedisp_f64_kernel: 16 waves x 4 trials");
     constexpr int K = 4, TT = 64 * K;
-    constexpr int kRecBytes = 4 * D * W;  // one channel's records, all waves: one DMA instruction
+    constexpr int kRecBytes = 2 * D * W;  // one channel's records, all waves (u16 words)
 
     const int wg = pu::xcd_remap(blockIdx.x, gridDim.x);
     const int dt = a.dt0 + wg % a.ndt;
@@ -133,7 +136,7 @@ dedisp_f64_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const in
     const int cover64 = (rowlen * 8 + 255) & ~255;  // bytes of a float64 row moved by DMA
     const int cover32 = (rowlen * 4 + 255) & ~255;  // bytes of a raw float32 row (its stride too)
     const int raw_bytes = kConv ? a.ncc * ((a.row_stride * 4 + 255) & ~255) : 0;
-    const int rec_slot = (a.ncc + 2) * kRecBytes;   // + 2 channels: the pipeline's read-ahead
+    const int rec_slot = (a.ncc + 2) * kRecBytes;   // + 2 channels: read-ahead, 256-byte DMA pieces
     unsigned char *raw = smem + 2 * buf_bytes;
     unsigned char *recs_lds = smem + 2 * buf_bytes + raw_bytes;
     const uint32_t smem_addr = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char *)smem;
@@ -145,17 +148,29 @@ dedisp_f64_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const in
         for (int k = 0; k < K; ++k) acc[d][k] = 0.0;
 
     const int32_t *base = base_tab + (size_t)dt * a.nchan;
-    const uint32_t *rec_g = rec_tab + (size_t)dt * a.nchan * (D * W);
+    const unsigned char *rec_g = reinterpret_cast<const unsigned char *>(rec_tab) + (size_t)dt * a.nchan * kRecBytes;
     const uint32_t *first_g = first_tab + (size_t)dt * a.nchan * W + wave;
     const Tin *data = reinterpret_cast<const Tin *>(a.data);
     const int nchunks = (a.nchan + a.ncc - 1) / a.ncc;
 
-    // this wave's rows of chunk k, ci = wave + W m, and their channels' records (it DMAs
-    // them and, for float32 inputs, converts the rows, so neither step needs a barrier of
-    // its own); rows into float64 buffer b (float64 input) or the raw buffer (float32)
+    // this wave's rows of chunk k, ci = wave + W m (it DMAs them and, for float32 inputs,
+    // converts them, so neither step needs a barrier of its own), rows into float64 buffer
+    // b (float64 input) or the raw buffer (float32); the chunk's records in 256-byte pieces
+    // (two channels each; the last piece may read past the records, into the first-window
+    // table that follows them)
     auto issue_dma = [&](int k, int b) {
         const int c0 = k * a.ncc;
         const int nc = min(a.ncc, a.nchan - c0);
+        for (int q = wave; 2 * q < nc; q += W) {
+            // the lane's byte offset made opaque here: hoisted out of the chunk loop, the
+            // per-lane 64-bit address (rec_g + lane) stayed live across the sum and spilled
+            uint32_t lane4 = 4u * (uint32_t)lane;
+            asm volatile("" : "+v"(lane4));
+            __builtin_amdgcn_global_load_lds((const void *)(rec_g + (size_t)(c0 + 2 * q) * kRecBytes + lane4),
+                                             (__attribute__((address_space(3))) void *)(recs_lds + (k & 1) * rec_slot +
+                                                                                         q * 2 * kRecBytes),
+                                             4, 0, 0);
+        }
         for (int ci = wave; ci < nc; ci += W) {
             const int c = c0 + ci;
             int start = ld_uniform(base + c) + t0;
@@ -166,15 +181,6 @@ dedisp_f64_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const in
                 dma_row_f32(raw + ci * cover32, row, start, cover32, n, small_n, lane);
             else
                 dma_row_f64(smem + b * buf_bytes + ci * chan_bytes, row, start, cover64, n, small_n, lane);
-            // the lane's byte offset made opaque here: hoisted out of the chunk loop, the
-            // per-lane 64-bit address (rec_g + lane) stayed live across the sum and spilled
-            uint32_t lane4 = 4u * (uint32_t)lane;
-            asm volatile("" : "+v"(lane4));
-            __builtin_amdgcn_global_load_lds((const void *)(reinterpret_cast<const char *>(rec_g + (size_t)c * (D * W)) +
-                                                            lane4),
-                                             (__attribute__((address_space(3))) void *)(recs_lds + (k & 1) * rec_slot +
-                                                                                         ci * kRecBytes),
-                                             4, 0, 0);
         }
     };
     auto convert = [&](int k, int b) {
@@ -208,24 +214,25 @@ dedisp_f64_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const in
         }
         if (!active) continue;
         const uint32_t rows = smem_addr + (uint32_t)(b * buf_bytes) + 8u * lane;
-        const uint32_t rows_m1 = rows - 1u;  // reload words are 1 + the byte offset
+        const uint32_t rows_m8 = rows - 8u;  // reload words are 1 + the offset in float64 elements
         // this wave's records of the chunk in LDS: channel ci at rec_v + ci * kRecBytes
-        uint32_t rec_v = smem_addr + (uint32_t)(2 * buf_bytes + raw_bytes + b * rec_slot + wave * 4 * D);
+        uint32_t rec_v = smem_addr + (uint32_t)(2 * buf_bytes + raw_bytes + b * rec_slot + wave * 2 * D);
         double w0[4], w1[4];
-        u32x4 vr;
+        u32x2 vr;
         // chunk start: channel c0's first window into w1 (state 0: trial 0 makes w1
         // current) and its record in flight
         prefetch_window<4>(w1, rows + ld_uniform(first_g + (size_t)c0 * W));
         prefetch_record(vr, rec_v);
-        // Channel code: trial 0 always reloads (w1 -> current, the next window prefetched
-        // into w0); trials 1..D-1 run a two-state machine (state S: wS current, the other
-        // buffer in flight) whose code for each (trial, state) is written out, so a reload is
-        // a wait + a swap of roles with no register moves.  The planner makes every channel's
-        // reload count even (a trial re-reading its predecessor's window where needed), so a
-        // channel always ends in state 0 with the next channel's first window in flight in
-        // w1: the code has one entry and one exit, and no state crosses channels.  Trial 0's
-        // wait also covers the channel's record (read during the previous channel's trial 0),
-        // which it moves into scalars before starting the next channel's read.
+        // Channel code: trial 0 always reloads; trials 1..D-1 run a two-state machine
+        // (state S: wS current, the other buffer in flight) whose code for each (trial,
+        // state) is written out, so a reload is a wait + a swap of roles with no register
+        // moves.  Channels are walked in pairs: the planner makes every pair's reload count
+        // even (a trial re-reading its predecessor's window where needed; a lone last
+        // channel's count on its own), so a pair starts and ends in state 0 with the next
+        // channel's first window in flight in w1 - one entry, one exit, no state variable;
+        // the pair's second channel has an entry for each state.  Trial 0's wait also covers
+        // the channel's record (read during the previous channel's trial 0), which it moves
+        // into scalars before starting the next channel's read.
 #define PU_F64_ADD(D_, W_)                                                                      \
     {                                                                                          \
         acc[D_][0] += W_[0];                                                                   \
@@ -236,9 +243,9 @@ dedisp_f64_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const in
     }
 #define PU_F64_TRIAL(P, R, D_, S_, WS, WO)                                                     \
     P##T##D_##_##S_:                                                                           \
-    if (R[D_] != 0u) {                                                                         \
+    if (PU_F64_WORD(R, D_) != 0u) {                                                            \
         wait_window<4>(WO);                                                                    \
-        prefetch_window<4>(WS, rows_m1 + R[D_]);                                               \
+        prefetch_window<4>(WS, rows_m8 + (PU_F64_WORD(R, D_) << 3));                           \
         PU_F64_ADD(D_, WO)                                                                     \
         goto P##T##D_##_flip_##S_;                                                             \
     }                                                                                          \
@@ -253,33 +260,52 @@ dedisp_f64_kernel(DedispArgs a, const int32_t *__restrict__ tile_first, const in
     goto P##T##N_##_1;                                                                         \
     P##T##D_##_flip_1:                                                                         \
     goto P##T##N_##_0;
-#define PU_F64_CHANNEL(P, R, RO)                                                               \
-    wait_window_record(w1, vr);                                                                \
-    const u32x4 R = readfirstlane4(vr);                                                        \
+        // trial 0 entered in state S (WS: the previous channel's last window, WO: this
+        // channel's first, in flight); continues at trial 1 in the other state
+#define PU_F64_ENTRY(P, R, RO, S_, WS, WO, N_)                                                 \
+    wait_window_record(WO, vr);                                                                \
+    R = readfirstlane2(vr);                                                                    \
     prefetch_record(vr, RO);                                                                   \
-    prefetch_window<4>(w0, rows_m1 + R[0]);                                                    \
-    PU_F64_ADD(0, w1)                                                                          \
-    goto P##T1_1;                                                                              \
+    prefetch_window<4>(WS, rows_m8 + (PU_F64_WORD(R, 0) << 3));                                \
+    PU_F64_ADD(0, WO)                                                                          \
+    goto P##T1_##N_;
+#define PU_F64_TRIALS(P, R)                                                                    \
     PU_F64_TRIAL(P, R, 1, 0, w0, w1) PU_F64_TRIAL(P, R, 1, 1, w1, w0) PU_F64_EDGES(P, 1, 2)    \
     PU_F64_TRIAL(P, R, 2, 0, w0, w1) PU_F64_TRIAL(P, R, 2, 1, w1, w0) PU_F64_EDGES(P, 2, 3)    \
-    PU_F64_TRIAL(P, R, 3, 0, w0, w1) PU_F64_TRIAL(P, R, 3, 1, w1, w0) PU_F64_EDGES(P, 3, 4)    \
-    P##T4_1: /* never reached (even reload counts); joins state 0 without a special exit */    \
-    goto P##T4_0;                                                                              \
-    P##T4_0:;
+    PU_F64_TRIAL(P, R, 3, 0, w0, w1) PU_F64_TRIAL(P, R, 3, 1, w1, w0) PU_F64_EDGES(P, 3, 4)
+        u32x2 ra, rb;
         // a real loop, not unrolled (LLVM unrolled round 5's first goto cycle ~20 times and
         // spilled)
 #pragma nounroll
-        for (int ci = 0; ci < nc; ++ci) {
-            PU_F64_CHANNEL(A, rec, rec_v + (ci + 1) * kRecBytes)
+        for (int ci = 0; ci < nc; ci += 2) {
+            PU_F64_ENTRY(A, ra, rec_v + (ci + 1) * kRecBytes, 0, w0, w1, 1)
+            PU_F64_TRIALS(A, ra)
+        AT4_0:
+            if (ci + 1 >= nc) goto chunk_done;
+            goto BE0;
+        AT4_1:  // (a lone last channel always ends in state 0)
+            if (ci + 1 >= nc) goto chunk_done;
+            goto BE1;
+        BE0:
+            PU_F64_ENTRY(B, rb, rec_v + (ci + 2) * kRecBytes, 0, w0, w1, 1)
+        BE1:
+            PU_F64_ENTRY(B, rb, rec_v + (ci + 2) * kRecBytes, 1, w1, w0, 0)
+            PU_F64_TRIALS(B, rb)
+        BT4_1:  // never reached (even pair reload counts): joins state 0 without an exit of its own
+            goto BT4_0;
+        BT4_0:;
         }
+    chunk_done:
         // the last prefetches (a re-read of the row base, or a record past the chunk's)
         // land before the next chunk's DMA can overwrite anything
         wait_window_record(w1, vr);
 #undef PU_F64_ADD
 #undef PU_F64_TRIAL
 #undef PU_F64_EDGES
-#undef PU_F64_CHANNEL
+#undef PU_F64_ENTRY
+#undef PU_F64_TRIALS
     }
+#undef PU_F64_WORD
     if (!active) return;
 
     if constexpr (STATS && !PLANE) {

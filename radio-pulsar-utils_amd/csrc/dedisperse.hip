@@ -549,7 +549,7 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
     // the allocation returns 0 (clamping them costs a VALU add per read - the reads then
     // cannot fold 256 u into the ds_read offset field - and was measured 1.8 ms slower at
     // C2, 20.2 vs 18.4 ms).
-    auto build_pass = [&](auto upc, const meta_t &m, int gs, int i0, int lim) {
+    auto build_pass = [&](auto upc, const meta_t &m, int gs, int i0, int lim, bool whole) {
         constexpr int UP = decltype(upc)::value;
         auto at = [&](int u) { return i0 + 64 * u + lane; };
         float r[UP];
@@ -611,8 +611,8 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
         // so does any pass whose UP chunks end inside the copy (4 i0 + 256 UP <= copy_bytes:
         // copy 1's stores end 4 bytes earlier than copy 0's) - round 5: C3's single pass per
         // slot (272 elements, UP = 5) no longer guards each store by a scalar compare + branch
-        // when its copy is 6 chunks long.
-        const bool whole = copy_bytes % (256 * UP) == 0 || 4 * i0 + 256 * UP <= copy_bytes;
+        // when its copy is 6 chunks long.  (whole: pass_whole(i0), decided by the caller - for
+        // the first pass once per tile.)
         asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(w0) : "memory");
         if (whole) {
 #pragma unroll
@@ -640,17 +640,31 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
     // slot over waves to balance the ~20 slots of a stage over 16 waves was measured
     // slower: 22.1 / 25.6 vs 20.2 ms for halves / thirds - fewer reads in flight per
     // pass, and the extra pass code spilled registers.)
+    auto pass_whole = [&](int i0) { return copy_bytes % (256 * U) == 0 || 4 * i0 + 256 * U <= copy_bytes; };
+    const bool whole0 = pass_whole(0);  // the first pass of every slot of the tile
     auto build = [&](const i32x4 st, const meta_t m0) {
         // the next slot's record is loaded a slot ahead (round 5: loaded on demand, its
-        // scalar-load latency stood in front of every slot after a wave's first)
-        meta_t m = m0;
-        for (int s = st.z + wave; s < st.w; s += W) {
-            const int sn = min(s + W, st.w - 1);
-            const meta_t mn = ld_uniform(reinterpret_cast<const meta_t *>(slots + (size_t)sn * MS));
+        // scalar-load latency stood in front of every slot after a wave's first), through a
+        // pointer stepped by W records: past the stage's last slot it reads the next stage's
+        // records or the table's padding (upload_sub: W records of zeros), never used.
+        // Every slot has a first pass (len >= TT): peeled, with the tile's whole0.
+        // Two slots per iteration with ping-pong records (rotating one record through a copy
+        // cost a dozen scalar moves per slot).
+        auto slot = [&](const meta_t &m) {
             const int len = m[0], gs = m[3];
             const int lim = (len + 63) & ~63;
-            for (int i0 = 0; i0 < len; i0 += 64 * U) build_pass(std::integral_constant<int, U>{}, m, gs, i0, lim);
-            m = mn;
+            build_pass(std::integral_constant<int, U>{}, m, gs, 0, lim, whole0);
+            for (int i0 = 64 * U; i0 < len; i0 += 64 * U)
+                build_pass(std::integral_constant<int, U>{}, m, gs, i0, lim, pass_whole(i0));
+        };
+        meta_t ma = m0;
+        const meta_t *mp = reinterpret_cast<const meta_t *>(slots) + (size_t)(st.z + wave + W);
+        for (int s = st.z + wave; s < st.w; s += 2 * W, mp += 2 * W) {
+            meta_t mb = ld_uniform(mp);
+            slot(ma);
+            if (s + W >= st.w) break;
+            ma = ld_uniform(mp + W);
+            slot(mb);
         }
     };
 
@@ -1036,7 +1050,7 @@ int ensure_lds(Kern kern, size_t bytes)
 int launch_f64(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s, bool tin_f32)
 {
     // records, then the first-window table (planner: one upload)
-    const uint32_t *first_off = p->d_rec8 + (size_t)p->ndt * p->nchan * kTPT;
+    const uint32_t *first_off = p->d_rec8 + (size_t)p->ndt * p->nchan * kTPT / 2;
     return pu_dd_launch_f64(tin_f32, plane, &a, sizeof a, p->lds_bytes, p->d_first, p->d_count, p->d_rowlen,
                             p->d_base, p->d_rec8, first_off, s, kF64Waves);
 }
@@ -1298,7 +1312,7 @@ int plan_channels(pu_plan *p, const int64_t *shifts, size_t budget)
     // (its stride: the row_stride's, as the kernel computes it), and two slots of window
     // records (one 256-byte DMA per channel, + 2 channels of read-ahead each)
     const int64_t raw_bytes = fsm && p->dtype == PU_F32 ? ((int64_t)p->row_stride * 4 + 255) / 256 * 256 : 0;
-    constexpr int64_t kRecChan = 4 * kTPT;
+    constexpr int64_t kRecChan = 2 * kTPT;  // u16 words
     const int64_t per_chan = nbuf * chan_bytes + raw_bytes + (fsm ? 2 * kRecChan : 0);
     const int64_t fixed = fsm ? 2 * 2 * kRecChan : 0;
     p->ncc = (int)std::max<int64_t>(1, std::min<int64_t>(nchan, (int64_t)((budget - fixed) / per_chan)));
@@ -1309,57 +1323,84 @@ int plan_channels(pu_plan *p, const int64_t *shifts, size_t budget)
     }
     // window records: per (tile, channel, wave) 8 x u16 = LDS byte offset of each
     // trial's window inside the row slot | (differs from the previous trial) << 15
-    // (dedisp_kernel); dedisp_f64_kernel: kF64Trials u32 per (tile, channel, wave), word d =
-    // 0 if trial d reads the window of trial d - 1, else 1 + the byte offset, from the
-    // chunk's row base, of the window to PREFETCH when trial d's becomes current (the next
-    // reloading trial's, after the channel's last reload the next channel's first, 0 + 1
-    // past the chunk: a harmless read of the row base); every channel's reload count is
-    // made even (trial 0 always reloads; an odd count gets the last non-reloading trial
-    // reloaded too, re-reading its predecessor's window) so that each channel starts and
-    // ends in the kernel's state 0.  After the records: per (tile, channel, wave) the byte
-    // offset of the channel's first window (read at chunk starts).
+    // (dedisp_kernel); dedisp_f64_kernel: kF64Trials u16 per (tile, channel, wave), word
+    // d = 0 if trial d reads the window of trial d - 1, else 1 + the offset in float64
+    // elements, from the chunk's row base, of the window to PREFETCH when trial d's becomes
+    // current (the next reloading trial's, after the channel's last reload the next
+    // channel's first, 0 + 1 past the chunk: a harmless read of the row base); the reload
+    // count of every channel pair the kernel walks (see below) is made even (trial 0 always
+    // reloads; an odd count gets a non-reloading trial reloaded too, re-reading its
+    // predecessor's window) so that each pair starts and ends in the kernel's state 0.
+    // After the records: per (tile, channel, wave) the byte offset of the channel's first
+    // window (read at chunk starts).
     const size_t copy_bytes = (size_t)p->row_stride * esz;
     std::vector<u32x4> rec(fsm ? 0 : (size_t)ndt * nchan * kWaves);
-    std::vector<uint32_t> rec8(fsm ? (size_t)ndt * nchan * kTPT + (size_t)ndt * nchan * kF64Waves : 0);
+    std::vector<uint32_t> rec8(fsm ? (size_t)ndt * nchan * kTPT / 2 + (size_t)ndt * nchan * kF64Waves : 0);
     int64_t f64_reads = 0;  // window reads of dedisp_f64_kernel, per launch and time tile
     if (fsm) {
-        if (p->ncc * chan_bytes + 1 >= (int64_t(1) << 31)) {
+        if (p->ncc * chan_bytes / 8 + 1 >= (int64_t(1) << 16)) {
             pu::set_error("pu_plan_create: float64 window records overflow");
             return PU_EUNSUPPORTED;
         }
         constexpr int FD = kF64Trials;
-        uint32_t *first8 = rec8.data() + (size_t)ndt * nchan * kTPT;
-        for (size_t t = 0; t < (size_t)ndt; ++t)
-            for (int64_t c = 0; c < nchan; ++c)
-                for (int w = 0; w < kF64Waves; ++w) {
-                    const int32_t *rr = rel.data() + (t * nchan + c) * kTPT + w * FD;
-                    const uint32_t cb = (uint32_t)((c % p->ncc) * chan_bytes);
-                    first8[(t * nchan + c) * kF64Waves + w] = cb + 8u * (uint32_t)rr[0];
-                    const bool nxt_ok = c + 1 < nchan && (c + 1) % p->ncc != 0;
-                    const uint32_t nxt_off =
-                        nxt_ok ? (uint32_t)(cb + chan_bytes + 8u * (uint32_t)rel[((t * nchan + c + 1) * kTPT) + w * FD])
-                               : 0u;
-                    bool reload[FD];
-                    int nre = 0;
-                    for (int d = 0; d < FD; ++d) {
-                        reload[d] = d == 0 || rr[d] != rr[d - 1];
-                        nre += reload[d];
-                    }
-                    if (nre & 1)
-                        for (int d = FD - 1; d > 0; --d)
-                            if (!reload[d]) {
-                                reload[d] = true;
-                                break;
-                            }
-                    uint32_t *r = rec8.data() + ((t * nchan + c) * kF64Waves + w) * FD;
-                    for (int d = 0; d < FD; ++d) {
-                        int e = d + 1;
-                        while (e < FD && !reload[e]) ++e;
-                        const uint32_t off = e < FD ? cb + 8u * (uint32_t)rr[e] : nxt_off;
-                        r[d] = reload[d] ? off + 1u : 0u;
-                        if (reload[d] && w * FD < count[t]) f64_reads += 1;
-                    }
+        uint32_t *first8 = rec8.data() + (size_t)ndt * nchan * kTPT / 2;
+        auto reloads = [&](size_t t, int64_t c, int w, bool (&re)[FD]) {
+            const int32_t *rr = rel.data() + (t * nchan + c) * kTPT + w * FD;
+            int nre = 0;
+            for (int d = 0; d < FD; ++d) {
+                re[d] = d == 0 || rr[d] != rr[d - 1];
+                nre += re[d];
+            }
+            return nre;
+        };
+        auto add_reload = [](bool (&re)[FD]) {  // the last non-reloading trial re-reads
+            for (int d = FD - 1; d > 0; --d)
+                if (!re[d]) {
+                    re[d] = true;
+                    return true;
                 }
+            return false;
+        };
+        auto emit = [&](size_t t, int64_t c, int w, const bool (&re)[FD]) {
+            const int32_t *rr = rel.data() + (t * nchan + c) * kTPT + w * FD;
+            const uint32_t cb = (uint32_t)((c % p->ncc) * chan_bytes);
+            first8[(t * nchan + c) * kF64Waves + w] = cb + 8u * (uint32_t)rr[0];
+            const bool nxt_ok = c + 1 < nchan && (c + 1) % p->ncc != 0;
+            const uint32_t nxt_off =
+                nxt_ok ? (uint32_t)(cb + chan_bytes + 8u * (uint32_t)rel[((t * nchan + c + 1) * kTPT) + w * FD]) : 0u;
+            uint32_t *r = rec8.data() + ((t * nchan + c) * kF64Waves + w) * (FD / 2);
+            for (int d = 0; d < FD; ++d) {
+                int e = d + 1;
+                while (e < FD && !re[e]) ++e;
+                const uint32_t off = e < FD ? cb + 8u * (uint32_t)rr[e] : nxt_off;
+                const uint32_t word = re[d] ? off / 8u + 1u : 0u;
+                r[d / 2] = d % 2 ? r[d / 2] | word << 16 : word;
+                if (re[d] && w * FD < count[t]) f64_reads += 1;
+            }
+        };
+        // the kernel walks each chunk's channels in pairs (a lone last one when the chunk's
+        // count is odd): a pair's reload count - a lone channel's - is made even, so every
+        // pair starts and ends in state 0 (the pair's second channel has an entry for each)
+        for (size_t t = 0; t < (size_t)ndt; ++t)
+            for (int64_t c0 = 0; c0 < nchan; c0 += p->ncc) {
+                const int64_t nc = std::min<int64_t>(p->ncc, nchan - c0);
+                for (int64_t ci = 0; ci < nc; ci += 2)
+                    for (int w = 0; w < kF64Waves; ++w) {
+                        bool ra[FD], rb[FD];
+                        int tot = reloads(t, c0 + ci, w, ra);
+                        const bool pair = ci + 1 < nc;
+                        if (pair) tot += reloads(t, c0 + ci + 1, w, rb);
+                        if (tot & 1) {
+                            const bool ok = (pair && add_reload(rb)) || add_reload(ra);
+                            if (!ok) {
+                                pu::set_error("pu_plan_create: float64 reload parity");  // unreachable
+                                return PU_EINVAL;
+                            }
+                        }
+                        emit(t, c0 + ci, w, ra);
+                        if (pair) emit(t, c0 + ci + 1, w, rb);
+                    }
+            }
     }
     for (size_t t = 0; t < (size_t)(fsm ? 0 : ndt); ++t)
         for (int64_t c = 0; c < nchan; ++c)
@@ -1792,6 +1833,9 @@ int upload_sub(pu_plan *p)
     if (!rc) rc = upload(&p->d_tiles, h.tiles);
     if (!rc) rc = upload(&p->d_tile_stages, h.tile_stages);
     if (!rc) rc = upload(&p->d_stages, h.stages);
+    // W (<= 16) records of padding: the kernel's build loads each wave's next slot record a
+    // slot ahead without clamping the index
+    h.slots.resize(h.slots.size() + (size_t)16 * slot_stride(8), 0);
     if (!rc) rc = upload(&p->d_slots, h.slots);
     if (!rc) rc = upload(&p->d_recs, h.recs);
     if (!rc && !h.base.empty()) rc = upload(&p->d_base, h.base);
