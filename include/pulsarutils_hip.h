@@ -248,6 +248,19 @@ int pu_ratio(double numerator, const double *x, int64_t n, double *out, void *st
 int pu_noisy_channels(const void *spec, int dtype, int64_t n, double mad_c, uint8_t *mask, int32_t *flag,
                       void *stream);
 
+/* measure_channel_variability's decision (pulsarutils/clean.py:114-133) certified from
+ * the means pass: means[nrows] (dtype PU_F32 / PU_F64: numpy's mean dtype) and
+ * moments[nrows][3] = (c, sum(x - c), sum((x - c)^2)) in float64 (pu_row_moments), n
+ * samples per row; mef, gam, u: the error factors of clean._certified_variability (the
+ * moments' relative error bound, numpy's std summation bound, the unit roundoff).
+ * mask[i] = std outside the quartile limits, or bad[i].  One workgroup, nrows <= 4096.
+ * *flag = 1 (mask not written, or not certified) for non-finite statistics, too few good
+ * channels for the reference's quartile indices, or a channel within its bound of a
+ * limit: the caller then computes numpy's std exactly (pu_row_sums mode 1). */
+int pu_variability_cert(const void *means, int dtype, const double *moments, int64_t nrows, int64_t n,
+                        double mef, double gam, double u, const uint8_t *bad, uint8_t *mask,
+                        int32_t *flag, void *stream);
+
 size_t pu_median_workspace_bytes(void);
 int pu_median(const double *x, int64_t n, double *out, void *ws, size_t ws_bytes, void *stream);
 

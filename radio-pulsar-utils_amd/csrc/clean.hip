@@ -1443,6 +1443,84 @@ noisy_channels_kernel(const T *__restrict__ spec, int n, double c, uint8_t *__re
     if (tid == 0) flag[0] = 0;
 }
 
+// ---------------------------------------------------------------- variability mask
+// measure_channel_variability's certified decision (clean.py:114-133) on the device: the
+// host restatement clean._certified_variability, step for step in float64 (same operation
+// order), from the means pass's numpy means (T) and shifted moments (c, s1, s2) per row:
+//   V = s2 - 2 dm s1 + n dm^2, dm = m - c;  eV = (s2 + 2 |dm| sqrt(n s2) + n dm^2) mef
+//   s_lo / s_hi = numpy's std bounds;  q1..q3 intervals = the k-th smallest s_lo / s_hi of
+//   the good channels (k = nrows/4, nrows/2, 3 nrows/4: the reference's indices);
+//   the limit intervals; a channel is decided when it is clear of both.
+// One workgroup, nrows <= kNoisyMax: bad channels' bounds are +inf in the two bitonic
+// sorts, so the k-th smallest of all is the k-th smallest good one.  *flag = 1 (mask not
+// written) for non-finite statistics, too few good channels, or any undecided channel:
+// the caller then runs the exact second pass.
+__device__ __forceinline__ void variability_bounds(double m, const double *mom, double nd, double mef, double gam,
+                                                   double u, double &lo, double &hi)
+{
+    const double c = mom[0], s1 = mom[1], s2 = mom[2];
+    const double dm = m - c;
+    const double V = (s2 - (2.0 * dm) * s1) + (nd * dm) * dm;
+    const double eV = ((s2 + (2.0 * fabs(dm)) * sqrt(nd * s2)) + (nd * dm) * dm) * mef + 1e-300;
+    lo = sqrt(fmax(V - eV, 0.0) * (1.0 - gam) / nd * (1.0 - u)) * (1.0 - u);
+    hi = sqrt((V + eV) * (1.0 + gam) / nd * (1.0 + u)) * (1.0 + u);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(1024)
+variability_cert_kernel(const T *__restrict__ means, const double *__restrict__ mom, int nrows, double nd,
+                        double mef, double gam, double u, const uint8_t *__restrict__ bad,
+                        uint8_t *__restrict__ mask, int32_t *__restrict__ flag)
+{
+    __shared__ double lo[kNoisyMax], hi[kNoisyMax];
+    __shared__ int gsum;
+    const int tid = threadIdx.x;
+    if (tid == 0) gsum = 0;
+    __syncthreads();
+    int nonfinite = 0, good = 0;
+    for (int i = tid; i < nrows; i += 1024) {
+        const double m = (double)means[i];
+        nonfinite |= !isfinite(m) || !isfinite(mom[3 * i]) || !isfinite(mom[3 * i + 1]) || !isfinite(mom[3 * i + 2]);
+        good += bad[i] == 0;
+    }
+    if (good) atomicAdd(&gsum, good);
+    const int any_nf = __syncthreads_or(nonfinite);  // (also orders the LDS adds before the read)
+    const int ngood = gsum;
+    if (any_nf || nrows / 4 * 3 >= ngood) {
+        if (tid == 0) flag[0] = 1;
+        return;
+    }
+    int m2 = 1;
+    while (m2 < nrows) m2 <<= 1;
+    for (int i = tid; i < m2; i += 1024) {
+        double a = INFINITY, b = INFINITY;
+        if (i < nrows && bad[i] == 0) variability_bounds((double)means[i], mom + 3 * i, nd, mef, gam, u, a, b);
+        lo[i] = a;
+        hi[i] = b;
+    }
+    __syncthreads();
+    bitonic_sort_lds(lo, m2);
+    bitonic_sort_lds(hi, m2);
+    const double a1 = lo[nrows / 4], b1 = hi[nrows / 4];
+    const double a2 = lo[nrows / 2], b2 = hi[nrows / 2];
+    const double a3 = lo[nrows / 4 * 3], b3 = hi[nrows / 4 * 3];
+    const double r = 4.0 * u * (b2 + 2.0 * (b3 - a1)) + 1e-300;
+    const double low_lo = (2.0 * a1 - b2) - r, low_hi = (2.0 * b1 - a2) + r;
+    const double hi_lo = (2.0 * a3 - b2) - r, hi_hi = (2.0 * b3 - a2) + r;
+    int unsure = 0;
+    for (int i = tid; i < nrows; i += 1024) {
+        double sl, sh;
+        variability_bounds((double)means[i], mom + 3 * i, nd, mef, gam, u, sl, sh);
+        const bool below = sh < low_lo, above = sl > hi_hi;
+        const bool sure = (below || sl >= low_hi) && (above || sh <= hi_lo);
+        const bool b = bad[i] != 0;
+        unsure |= !b && !sure;
+        mask[i] = (below || above || b) ? 1 : 0;
+    }
+    const int any_unsure = __syncthreads_or(unsure);
+    if (tid == 0) flag[0] = any_unsure ? 1 : 0;
+}
+
 __global__ void ratio_dev_kernel(const double *__restrict__ num, const double *__restrict__ x, int64_t n,
                                  double *__restrict__ out)
 {
@@ -1902,6 +1980,25 @@ int pu_median(const double *x, int64_t n, double *out, void *ws, size_t ws_bytes
         hipLaunchKernelGGL(median_hist_kernel, dim3(grid), dim3(256), 0, s, x, n, st, hist, p);
     hipLaunchKernelGGL(median_final_kernel, dim3(1), dim3(256), 0, s, st, hist, n, out);
     return pu::launch_check("median_kernels");
+}
+
+int pu_variability_cert(const void *means, int dtype, const double *moments, int64_t nrows, int64_t n, double mef,
+                        double gam, double u, const uint8_t *bad, uint8_t *mask, int32_t *flag, void *stream)
+{
+    PU_REQUIRE(means && moments && bad && mask && flag, "pu_variability_cert: NULL pointer");
+    PU_REQUIRE(nrows >= 1 && nrows <= kNoisyMax, "pu_variability_cert: nrows = %lld outside [1, %d]",
+               (long long)nrows, kNoisyMax);
+    PU_REQUIRE(n >= 1, "pu_variability_cert: n must be positive");
+    PU_REQUIRE(dtype == PU_F32 || dtype == PU_F64, "pu_variability_cert: means must be float32 or float64");
+    if (dtype == PU_F32)
+        hipLaunchKernelGGL(variability_cert_kernel<float>, dim3(1), dim3(1024), 0, pu::as_stream(stream),
+                           reinterpret_cast<const float *>(means), moments, (int)nrows, (double)n, mef, gam, u, bad,
+                           mask, flag);
+    else
+        hipLaunchKernelGGL(variability_cert_kernel<double>, dim3(1), dim3(1024), 0, pu::as_stream(stream),
+                           reinterpret_cast<const double *>(means), moments, (int)nrows, (double)n, mef, gam, u, bad,
+                           mask, flag);
+    return pu::launch_check("variability_cert_kernel");
 }
 
 int pu_noisy_channels(const void *spec, int dtype, int64_t n, double mad_c, uint8_t *mask, int32_t *flag,

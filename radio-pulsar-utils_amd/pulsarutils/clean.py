@@ -72,6 +72,7 @@ def _row_sums(x, mode, center=None, scale=None, divisor=0.0):
 
 
 _MEANS = [None]  # (weakref to the tensor, its version counter, the means, the shifted moments)
+_VAR = [None]    # (weakref to the tensor, its version counter, the bad mask, the variability mask)
 
 
 def _row_moments(x):
@@ -89,30 +90,31 @@ def _row_moments(x):
     return means, mom
 
 
-def _cached_stats(x, host=False):
-    """(means, moments) of ``x`` from the cache, or one pu_row_moments pass (cached).
-
-    The pass also starts an asynchronous copy of [means | moments] (float64, nrows x 4)
-    to pinned host memory, so that measure_channel_variability - which needs them on the
-    host - usually finds them there after get_noisier_channels' own synchronisation
-    instead of waiting for a copy of its own.  ``host=True`` returns that host array
-    (waiting for the copy) in place of the device moments."""
+def _cached_stats(x):
+    """(means, moments) of ``x`` from the cache, or one pu_row_moments pass (cached)."""
     import weakref
-    t = _hip.torch()
     c = _MEANS[0]
     if not (c is not None and c[0]() is x and c[1] == (x._version, x.data_ptr())):
         m, mom = _row_moments(x)
-        both = t.cat([m.to(t.float64)[:, None], mom], dim=1)
-        hbuf = t.empty(both.shape, dtype=t.float64, pin_memory=True)
-        hbuf.copy_(both, non_blocking=True)
-        ev = t.cuda.Event()
-        ev.record()
-        c = (weakref.ref(x), (x._version, x.data_ptr()), m, mom, hbuf, ev)
+        c = (weakref.ref(x), (x._version, x.data_ptr()), m, mom)
         _MEANS[0] = c
-    if host:
-        c[5].synchronize()
-        return c[2], c[4].numpy()
     return c[2], c[3]
+
+
+def _variability_args(means, n):
+    """pu_variability_cert's error factors (as _certified_variability)."""
+    u = 2.0 ** -24 if means.dtype == _hip.torch().float32 else 2.0 ** -53
+    return moment_error_factor(n), (35 + -(-int(n) // 8192) + 4) * u, u
+
+
+def _launch_variability(x, bad_dev, out_mask, out_flag):
+    """Queue the device variability decision of ``x`` with the uint8 device mask ``bad_dev``."""
+    means, mom = _cached_stats(x)
+    nrows, n = x.shape
+    mef, gam, u = _variability_args(means, n)
+    _hip.check(_hip.lib().pu_variability_cert(_hip.ptr(means), _hip.dtype_code(means.dtype), _hip.ptr(mom), nrows, n,
+                                              mef, gam, u, _hip.ptr(bad_dev), out_mask, out_flag,
+                                              _hip.stream_ptr()), "pu_variability_cert")
 
 
 def channel_means_device(x):
@@ -134,6 +136,7 @@ def channel_means_device(x):
 def invalidate_channel_means():
     """Forget the cached channel means (see :func:`channel_means_device`)."""
     _MEANS[0] = None
+    _VAR[0] = None
 
 
 def channel_variances_device(x, means=None):
@@ -167,20 +170,34 @@ def get_noisier_channels(array):
 
     The decision runs on the device (pu_noisy_channels: medfilt, ref_mad and the
     comparison in numpy's dtypes and order) and only the mask comes back; a spec with
-    NaN / inf, or more than 4096 channels, is decided on the host by numpy / scipy."""
+    NaN / inf, or more than 4096 channels, is decided on the host by numpy / scipy.
+    In the same read-back: measure_channel_variability's decision for this mask
+    (pu_variability_cert, queued behind it), kept for the same unmodified tensor - the
+    usual next call, measure_channel_variability(x, badchans_mask=<this mask>), then
+    needs no GPU work and no synchronisation of its own."""
+    import weakref
     x = _hip.to_device(array)
     spec_d = channel_means_device(x)
     n = spec_d.numel()
     if 2 <= n <= _NOISY_MAX:
         t = _hip.torch()
         off = (n + 3) & ~3
-        res = t.empty(off + 4, dtype=t.uint8, device=spec_d.device)  # mask, then the int32 flag
+        # [noisy mask | its flag | variability mask | its flag]
+        res = t.empty(2 * (off + 4), dtype=t.uint8, device=spec_d.device)
+        base = res.data_ptr()
         _hip.check(_hip.lib().pu_noisy_channels(_hip.ptr(spec_d), _hip.dtype_code(spec_d.dtype), n, float(MAD_C),
-                                                _hip.ptr(res), res.data_ptr() + off, _hip.stream_ptr()),
+                                                base, base + off, _hip.stream_ptr()),
                    "pu_noisy_channels")
+        # (when the noisy flag is set the mask is unwritten: the variability result is
+        # then discarded)
+        _launch_variability(x, res[:n], base + off + 4, base + 2 * off + 4)
         h = _host(res)
         if not h[off:off + 4].view(np.int32)[0]:
-            return h[:n].astype(bool)
+            mask = h[:n].astype(bool)
+            if not h[2 * off + 4:2 * off + 8].view(np.int32)[0]:
+                _VAR[0] = (weakref.ref(x), (x._version, x.data_ptr()), mask.copy(),
+                           h[off + 4:off + 4 + n].astype(bool))
+            return mask
     spec = _host(spec_d)
     smooth_spec = medfilt(spec, 7)
     return spec > smooth_spec + 5 * ref_mad(spec)
@@ -249,19 +266,37 @@ def measure_channel_variability(array, badchans_mask=None):
 
     Quartile positions use the full channel count, as in the reference (an
     IndexError when too many channels are masked is the reference behaviour).
-    The decisions are certified from the shifted moments of the means pass
-    (_certified_variability, no second read pass); only when one is within its
-    rounding bound is numpy's std computed exactly (a second pass).
+    The decisions are certified from the shifted moments of the means pass on the
+    device (pu_variability_cert; computed ahead by get_noisier_channels for its own
+    mask), no second read pass; only when one is within its rounding bound is numpy's
+    std computed exactly (a second pass).  More than 4096 channels: the same
+    certification on the host (_certified_variability).
     """
     x = _hip.to_device(array)
     if badchans_mask is None:
         badchans_mask = np.zeros(x.shape[0], dtype=bool)
     badchans_mask = np.asarray(badchans_mask, dtype=bool)
     t = _hip.torch()
-    means, both = _cached_stats(x, host=True)  # [means (exact in float64) | moments] on the host
-    mask = _certified_variability(both[:, 0], both[:, 1:], x.shape[1], means.dtype == t.float32, badchans_mask)
-    if mask is not None:
-        return mask
+    nrows = x.shape[0]
+    v = _VAR[0]
+    if (v is not None and v[0]() is x and v[1] == (x._version, x.data_ptr())
+            and np.array_equal(v[2], badchans_mask)):
+        return v[3].copy()
+    means, mom = _cached_stats(x)
+    if nrows <= _NOISY_MAX:
+        off = (nrows + 3) & ~3
+        bad_np = np.ascontiguousarray(badchans_mask).astype(np.uint8)
+        bad = t.from_numpy(bad_np).pin_memory().to(x.device, non_blocking=True)
+        res = t.empty(off + 4, dtype=t.uint8, device=x.device)
+        _launch_variability(x, bad, res.data_ptr(), res.data_ptr() + off)
+        h = _host(res)
+        if not h[off:off + 4].view(np.int32)[0]:
+            return h[:nrows].astype(bool)
+    else:
+        mask = _certified_variability(_host(means).astype(np.float64), _host(mom), x.shape[1],
+                                      means.dtype == t.float32, badchans_mask)
+        if mask is not None:
+            return mask
     spec = np.sqrt(_host(channel_variances_device(x, means)))
     ordered = np.sort(spec[~badchans_mask])
     q1 = ordered[spec.size // 4]

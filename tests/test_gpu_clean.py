@@ -493,6 +493,74 @@ def test_variability_one_pass_and_fallback(gpu):
         C.channel_variances_device = orig
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.uint8, np.float64])
+@pytest.mark.parametrize("nchan,n", [(4, 5000), (100, 12345), (1024, 16384), (4096, 2048)])
+def test_variability_cert_device_matches_host(gpu, dtype, nchan, n):
+    """pu_variability_cert (round 5) = the host restatement _certified_variability: the
+    same certified-or-not outcome and, when certified, the same mask (which then equals
+    the reference's decision: checked against the oracle too); masks with bad channels,
+    too many bad channels (not certifiable), a channel forced onto a limit."""
+    from pulsarutils import _hip
+    import torch
+    rng = np.random.default_rng(nchan + n)
+    x = rng.normal(100.0, 5.0, (nchan, n)) * rng.uniform(0.7, 1.4, nchan)[:, None]
+    x = (np.clip(x, 0, 255) if dtype == np.uint8 else x).astype(dtype)
+    cases = [np.zeros(nchan, bool), rng.random(nchan) < 0.1, rng.random(nchan) < 0.3]
+    if nchan >= 8:
+        many = np.ones(nchan, bool)
+        many[: nchan // 4] = False  # nchan // 4 * 3 >= good: the reference's indices fail
+        cases.append(many)
+    xd = _hip.to_device(x)
+    C.invalidate_channel_means()
+    means, mom = C._cached_stats(xd)
+    off = (nchan + 3) & ~3
+    for bad in cases:
+        host = C._certified_variability(means.cpu().numpy().astype(np.float64), mom.cpu().numpy(), n,
+                                        means.dtype == torch.float32, bad)
+        badd = torch.from_numpy(bad.astype(np.uint8)).to(xd.device)
+        res = torch.zeros(off + 4, dtype=torch.uint8, device=xd.device)
+        C._launch_variability(xd, badd, res.data_ptr(), res.data_ptr() + off)
+        h = res.cpu().numpy()
+        flag = int(h[off:off + 4].view(np.int32)[0])
+        assert flag == (host is None), (flag, host is None)
+        if host is not None:
+            np.testing.assert_array_equal(h[:nchan].astype(bool), host)
+            if bad.sum() < nchan // 2:
+                np.testing.assert_array_equal(host, co.channel_variability(x, badchans_mask=bad))
+
+
+@pytest.mark.parametrize("dt", ["f32", "u8"])
+def test_masks_one_readback_on_device_tensor(gpu, golden, dt):
+    """get_noisier_channels on a device tensor also decides measure_channel_variability
+    for its own mask (one read-back for both); the next call with that mask returns the
+    kept result without a GPU call, a different mask or a modified tensor recomputes -
+    all equal to the reference's goldens / oracle."""
+    from pulsarutils import _hip
+    arrays, meta = golden
+    x = synth.rfi_filterbank_np(CONFIGS["C4"], dtype=dt)
+    xd = _hip.to_device(x)
+    C.invalidate_channel_means()
+    bad = C.get_noisier_channels(xd)
+    np.testing.assert_array_equal(bad, arrays[f"c4{dt}_noisier"])
+    lib = _hip.lib()
+    calls = []
+    orig = C._launch_variability
+    C._launch_variability = lambda *a, **k: (calls.append(1), orig(*a, **k))[1]
+    try:
+        got = C.measure_channel_variability(xd, badchans_mask=bad)
+        assert not calls  # decided with get_noisier_channels' read-back
+        np.testing.assert_array_equal(got, arrays[f"c4{dt}_variability_masked"])
+        other = bad.copy()
+        other[0] = not other[0]
+        got2 = C.measure_channel_variability(xd, badchans_mask=other)
+        assert calls
+        np.testing.assert_array_equal(got2, co.channel_variability(x, badchans_mask=other))
+        np.testing.assert_array_equal(C.measure_channel_variability(xd), arrays[f"c4{dt}_variability"])
+    finally:
+        C._launch_variability = orig
+    del lib
+
+
 @pytest.mark.parametrize("n,sigma", [(262144, 101), (262145, 101), (262143, 55), (1, 1), (7, 2), (1000, 3),
                                      (3 * 262144 + 17, 101), (2 * 262144, 0.2), (12345, 600)])
 def test_light_curve_factor(gpu, n, sigma):
