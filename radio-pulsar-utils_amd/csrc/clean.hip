@@ -1381,6 +1381,42 @@ __device__ void bitonic_sort_lds(T *v, int m)  // m: power of two, 1024 threads
         }
 }
 
+// Ascending sort of v[0, m) (m a power of two) by 1024 threads.  m <= 1024 (round 5): one
+// element per thread in a register, +inf padding to 1024; the 45 of the 55 bitonic steps
+// whose partner is in the same wave exchange by __shfl_xor (no barrier), the 10 with a
+// partner in another wave through v itself (two alternating halves of v[0, 2048): one
+// barrier per step; v must hold 2048 elements).  Larger m: bitonic_sort_lds.  The values
+// are finite or +inf (the callers check), so min / max by comparison are exact.
+__device__ void sort_1024(double *v, int m)
+{
+    if (m > 1024) {
+        bitonic_sort_lds(v, m);
+        return;
+    }
+    const int i = threadIdx.x;
+    double x = i < m ? v[i] : INFINITY;
+    __syncthreads();  // every thread has its element before v is reused as the exchange
+    int half = 0;
+    for (int k = 2; k <= 1024; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            double y;
+            if (j >= 64) {
+                double *ex = v + 1024 * half;
+                ex[i] = x;
+                __syncthreads();
+                y = ex[i ^ j];
+                half ^= 1;  // the next exchange writes the other half: no second barrier
+            } else {
+                y = __shfl_xor(x, j, 64);
+            }
+            const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+            x = keep_min ? (y < x ? y : x) : (y > x ? y : x);
+        }
+    __syncthreads();  // every exchange read is done
+    if (i < m) v[i] = x;
+    __syncthreads();
+}
+
 template <typename T>
 __device__ T median_sorted(const T *v, int cnt)  // numpy: middle element / mean of the two
 {
@@ -1412,13 +1448,13 @@ noisy_channels_kernel(const T *__restrict__ spec, int n, double c, uint8_t *__re
     // the differences in T (np.diff of the T spectrum), then exactly widened to float64
     for (int i = tid; i < m; i += 1024) ev[i] = i < n - 1 ? (double)T(sp[i + 1] - sp[i]) : INFINITY;
     __syncthreads();
-    bitonic_sort_lds(ev, m);
+    sort_1024(ev, m);
     const double med = median_sorted(ev, n - 1);
     __syncthreads();  // every thread has read the median before ev is overwritten
     for (int i = tid; i < m; i += 1024)
         ev[i] = i < n - 1 ? fabs((double)T(sp[i + 1] - sp[i]) - med) / c : INFINITY;
     __syncthreads();
-    bitonic_sort_lds(ev, m);
+    sort_1024(ev, m);
     const double rm = median_sorted(ev, n - 1) / 1.4142135623730951;  // np.sqrt(2)
     const double thr = 5.0 * rm;
     for (int i = tid; i < n; i += 1024) {
@@ -1499,8 +1535,8 @@ variability_cert_kernel(const T *__restrict__ means, const double *__restrict__ 
         hi[i] = b;
     }
     __syncthreads();
-    bitonic_sort_lds(lo, m2);
-    bitonic_sort_lds(hi, m2);
+    sort_1024(lo, m2);
+    sort_1024(hi, m2);
     const double a1 = lo[nrows / 4], b1 = hi[nrows / 4];
     const double a2 = lo[nrows / 2], b2 = hi[nrows / 2];
     const double a3 = lo[nrows / 4 * 3], b3 = hi[nrows / 4 * 3];

@@ -64,7 +64,7 @@ def _row_sums(x, mode, center=None, scale=None, divisor=0.0):
     acc_f32 = code == _hip.PU_F32 and mode in (0, 1)
     nrows, n = x.shape
     out = t.empty(nrows, dtype=t.float32 if acc_f32 else t.float64, device=x.device)
-    ws = t.empty(max(16, _hip.lib().pu_row_sums_workspace_bytes(nrows, n)), dtype=t.uint8, device=x.device)
+    ws = _workspace(x.device, _hip.lib().pu_row_sums_workspace_bytes(nrows, n))
     _hip.check(_hip.lib().pu_row_sums(_hip.ptr(x), code, nrows, n, x.stride(0), mode, _hip.ptr(center),
                                       _hip.ptr(scale), float(divisor), _hip.ptr(out), _hip.ptr(ws), ws.numel(),
                                       _hip.stream_ptr()), "pu_row_sums")
@@ -75,6 +75,21 @@ _MEANS = [None]  # (weakref to the tensor, its version counter, the means, the s
 _VAR = [None]    # (weakref to the tensor, its version counter, the bad mask, the variability mask)
 
 
+_WS = {}  # device -> scratch of pu_row_moments (stream-ordered: one stream per device here)
+
+
+def _workspace(dev, nbytes):
+    """A scratch buffer of at least ``nbytes`` on ``dev``, kept between calls: its users are
+    queued on torch's current stream, which orders every reuse after the previous one."""
+    t = _hip.torch()
+    key = (str(dev), _hip.stream_ptr().value)
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = t.empty(max(nbytes, 16), dtype=t.uint8, device=dev)
+        _WS[key] = buf
+    return buf
+
+
 def _row_moments(x):
     """pu_row_moments: numpy's x.mean(1) (f32 for f32 input, else f64) and, from the same
     read pass, per row (c, sum(x - c), sum((x - c)^2)) in float64 with c = x[r, 0]."""
@@ -83,7 +98,7 @@ def _row_moments(x):
     acc_f32 = _hip.dtype_code(x.dtype) == _hip.PU_F32
     means = t.empty(nrows, dtype=t.float32 if acc_f32 else t.float64, device=x.device)
     mom = t.empty((nrows, 3), dtype=t.float64, device=x.device)
-    ws = t.empty(_hip.lib().pu_row_moments_workspace_bytes(nrows, n), dtype=t.uint8, device=x.device)
+    ws = _workspace(x.device, _hip.lib().pu_row_moments_workspace_bytes(nrows, n))
     _hip.check(_hip.lib().pu_row_moments(_hip.ptr(x), _hip.dtype_code(x.dtype), nrows, n, x.stride(0),
                                          _hip.ptr(means), _hip.ptr(mom), _hip.ptr(ws), ws.numel(),
                                          _hip.stream_ptr()), "pu_row_moments")
@@ -177,7 +192,7 @@ def get_noisier_channels(array):
     needs no GPU work and no synchronisation of its own."""
     import weakref
     x = _hip.to_device(array)
-    spec_d = channel_means_device(x)
+    spec_d = _cached_stats(x)[0]  # (read only here: no defensive copy)
     n = spec_d.numel()
     if 2 <= n <= _NOISY_MAX:
         t = _hip.torch()

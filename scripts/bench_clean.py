@@ -6,6 +6,7 @@ given), each device step of the reference's cleaning pass on a resident
 1024 x 2^18 RFI-heavy filterbank:
   means     channel_means_device      (clean.py:58-67 spectrum)
   var       channel_variances_device  (clean.py:114-133 np.std)
+  masks     get_noisier_channels + measure_channel_variability (clean.py:58-67, 114-133)
   renorm    renormalize_device(cut_outliers=True) (clean.py:70-111; includes the
             host median / threshold round trips the reference formula needs)
 and prints one JSON line per step with algorithmic HBM bytes and GB/s vs the
@@ -49,6 +50,9 @@ steps = {
     "var": (lambda: clean.channel_variances_device(x, means), plane),
     # col means (1 read) + factor-weighted row sums (1 read + factor) + apply
     # (1 read + float64 write + column means); small 1-D passes counted too
+    # both channel masks from scratch (bench.py's masks step): one read pass + decisions
+    "masks": (lambda: (clean.invalidate_channel_means(),
+                       clean.measure_channel_variability(x, badchans_mask=clean.get_noisier_channels(x)))[1], plane),
     "renorm": (lambda: clean.renormalize_device(x, bad, cut_outliers=True, out=out),
                3 * plane + nchan * n * 8 + 6 * n * 8),
 }
