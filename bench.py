@@ -351,6 +351,9 @@ def main():
                     help="with --scaling strong on one GPU: search only rank 0's slice of an N-way split "
                          "(e.g. --config C3 --scaling strong --shard 8: the 625-trial shard of the 8-GPU run)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ref", action="store_true",
+                    help="N > 1 strong split: skip the one-GPU run of the same workload on rank 0")
+    ap.add_argument("--ref-steps", type=int, default=1)
     ap.add_argument("--cpu-trials", type=int, default=400)
     ap.add_argument("--no-clean", action="store_true")
     ap.add_argument("--clean-steps", type=int, default=5)
@@ -532,6 +535,32 @@ def main():
                                          "peak; the subband decomposition executes group x fewer adds, and the "
                                          "unit that binds it is the LDS array: lds_frac"})
 
+    # N > 1, strong split: the same whole workload on rank 0's GPU alone (untimed by the
+    # step; the other ranks wait), so the line carries its own one-GPU reference - the N = 1
+    # headline is C2 (configs[1]), a different workload
+    ref1 = None
+    if pipelined and not args.no_ref:
+        if rank == 0:
+            log("one-GPU reference (the whole grid on rank 0) ...")
+            sh_all = _hip.shift_table(cfg.nchan, dms_all, cfg.start_freq, cfg.bandwidth, cfg.tsamp)
+            plan1 = _hip.Plan(_hip.dtype_code(x.dtype), acc, cfg.nchan, cfg.nsamples, sh_all)
+            ws1 = torch.empty(plan1.workspace_bytes, dtype=torch.uint8, device=dev)
+            plan1.search(x, workspace=ws1)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(args.ref_steps):
+                plan1.search(x, workspace=ws1)
+            torch.cuda.synchronize()
+            ms1 = (time.perf_counter() - t1) / args.ref_steps * 1e3
+            ref1 = {"what": "the same workload (all trials, the resident filterbank, no exchange) searched on "
+                            "rank 0's GPU alone, after the timed steps", "ms_per_step": ms1,
+                    "value": total_samples / (ms1 / 1e3), "steps": args.ref_steps,
+                    "speedup": (total_samples / (ms_per_step / 1e3)) / (total_samples / (ms1 / 1e3)),
+                    "efficiency": ms1 / ms_per_step / world}
+            del plan1, ws1
+            torch.cuda.empty_cache()
+        dist.barrier()
+
     f64 = None
     if rank == 0 and world == 1 and not args.no_acc_f64 and args.acc == "native" and cfg.dtype != "f64":
         log("acc_f64 ...")
@@ -591,6 +620,8 @@ def main():
             line["c3_strong"] = c3
         if bcast is not None:
             line["multi_gpu"] = bcast
+        if ref1 is not None:
+            line["single_gpu_same_workload"] = ref1
         line["build"] = _hip.build_info()  # was the library built from the sources shipped with it
         print(json.dumps(line), flush=True)
     if world > 1:
