@@ -63,6 +63,7 @@ __device__ __forceinline__ uint64_t stamp()
 #endif
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 // Channel-mode window reads: J x ds_read_b64 at 512-byte strides (inline asm: hipcc

@@ -78,8 +78,6 @@ __device__ __forceinline__ void dma_row_f64(unsigned char *dst, const double *ro
     }
 }
 
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-
 // One channel's record (D = 4 u16, uniform across the wave) read from LDS into VGPRs,
 // issued without a wait (ds_read_b64: 2 LDS cycles, a 16-byte record's ds_read_b128 takes
 // 4); wait_window_record() waits for it together with a window.
