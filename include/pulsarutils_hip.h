@@ -261,6 +261,16 @@ int pu_variability_cert(const void *means, int dtype, const double *moments, int
                         double mef, double gam, double u, const uint8_t *bad, uint8_t *mask,
                         int32_t *flag, void *stream);
 
+/* get_noisier_channels and then measure_channel_variability(badchans_mask=<that mask>)
+ * (pulsarutils/clean.py:58-67, then :114-133) in ONE launch: pu_noisy_channels' decision on
+ * spec = means (noisy[nrows], *noisy_flag), then pu_variability_cert's with the noisy mask
+ * as bad (var[nrows], *var_flag), same arguments and flag meanings as those two calls
+ * (mad_c: pu_noisy_channels'; mef, gam, u: pu_variability_cert's).  One workgroup,
+ * 2 <= nrows <= 1024; a non-finite spec sets both flags. */
+int pu_channel_masks(const void *means, int dtype, const double *moments, int64_t nrows, int64_t n,
+                     double mad_c, double mef, double gam, double u, uint8_t *noisy,
+                     int32_t *noisy_flag, uint8_t *var, int32_t *var_flag, void *stream);
+
 size_t pu_median_workspace_bytes(void);
 int pu_median(const double *x, int64_t n, double *out, void *ws, size_t ws_bytes, void *stream);
 

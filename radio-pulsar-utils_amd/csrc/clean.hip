@@ -1381,12 +1381,99 @@ __device__ void bitonic_sort_lds(T *v, int m)  // m: power of two, 1024 threads
         }
 }
 
-// Ascending sort of v[0, m) (m a power of two) by 1024 threads.  m <= 1024 (round 5): one
-// element per thread in a register, +inf padding to 1024; the 45 of the 55 bitonic steps
-// whose partner is in the same wave exchange by __shfl_xor (no barrier), the 10 with a
-// partner in another wave through v itself (two alternating halves of v[0, 2048): one
-// barrier per step; v must hold 2048 elements).  Larger m: bitonic_sort_lds.  The values
-// are finite or +inf (the callers check), so min / max by comparison are exact.
+// x of lane (lane ^ J) within the wave, on the VALU (no LDS round trip): DPP quad
+// permutes for J = 1, 2, row rotations for 4, 8 (J = 4: rotations by 4 and 12, the one
+// whose source is lane ^ 4 picked per lane - sel4, computed once by the caller from the
+// same rotation of the lane ids), the gfx950 permlane swaps for 16, 32 (the pair returns
+// rows / halves exchanged: lanes in the upper row / half take the first result).
+template <int J>
+__device__ __forceinline__ double lane_xor(double x, int lane, bool sel4)
+{
+    const uint64_t u = __builtin_bit_cast(uint64_t, x);
+    uint32_t w[2] = {(uint32_t)u, (uint32_t)(u >> 32)};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int v = (int)w[h];
+        if constexpr (J == 1) {
+            w[h] = (uint32_t)__builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+        } else if constexpr (J == 2) {
+            w[h] = (uint32_t)__builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+        } else if constexpr (J == 4) {
+            const int a = __builtin_amdgcn_mov_dpp(v, 0x124, 0xf, 0xf, false);  // row_ror:4
+            const int b = __builtin_amdgcn_mov_dpp(v, 0x12C, 0xf, 0xf, false);  // row_ror:12
+            w[h] = (uint32_t)(sel4 ? a : b);
+        } else if constexpr (J == 8) {
+            w[h] = (uint32_t)__builtin_amdgcn_mov_dpp(v, 0x128, 0xf, 0xf, false);  // row_ror:8
+        } else if constexpr (J == 16) {
+            const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+            w[h] = (lane & 16) ? (uint32_t)r[0] : (uint32_t)r[1];
+        } else {
+            static_assert(J == 32, "lane_xor: J = 1 .. 32");
+            const auto r = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+            w[h] = (lane & 32) ? (uint32_t)r[0] : (uint32_t)r[1];
+        }
+    }
+    return __builtin_bit_cast(double, (uint64_t)w[0] | ((uint64_t)w[1] << 32));
+}
+
+// the in-wave bitonic steps j = J, J/2, .., 1 of merge size k (lane_xor exchanges)
+template <int J>
+__device__ __forceinline__ void bitonic_wave_steps(double &x, int i, int k, int lane, bool sel4)
+{
+    const double y = lane_xor<J>(x, lane, sel4);
+    const bool keep_min = ((i & J) == 0) == ((i & k) == 0);
+    x = keep_min ? (y < x ? y : x) : (y > x ? y : x);
+    if constexpr (J > 1) bitonic_wave_steps<J / 2>(x, i, k, lane, sel4);
+}
+
+// NV independent ascending sorts over the 1024 threads of the workgroup, one value of each
+// per thread in x[q] (thread i ends with the i-th smallest of sort q), the sorts sharing
+// every barrier.  Bitonic: the 45 of the 55 steps whose partner is in the same wave
+// exchange on the VALU (lane_xor: DPP and permlane swaps, no barrier; round 5 first:
+// __shfl_xor, an LDS permute per step), the 10 with a partner in another wave through ex
+// (NV x 2048 doubles of LDS, two alternating halves per sort: one barrier per step).  ex
+// must be free on entry; the caller synchronises before reusing it.  The values are finite
+// or +inf (the callers check), so min / max by comparison are exact.
+template <int NV>
+__device__ void sort_regs_1024(double (&x)[NV], double *ex)
+{
+    const int i = threadIdx.x;
+    const int lane = i & 63;
+    // the lane whose value row_ror:4 brings (whatever the rotation's direction)
+    const bool sel4 = __builtin_amdgcn_mov_dpp(lane, 0x124, 0xf, 0xf, false) == (lane ^ 4);
+    // merge sizes 2 .. 64 inside each wave
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+        bitonic_wave_steps<1>(x[q], i, 2, lane, sel4);
+        bitonic_wave_steps<2>(x[q], i, 4, lane, sel4);
+        bitonic_wave_steps<4>(x[q], i, 8, lane, sel4);
+        bitonic_wave_steps<8>(x[q], i, 16, lane, sel4);
+        bitonic_wave_steps<16>(x[q], i, 32, lane, sel4);
+        bitonic_wave_steps<32>(x[q], i, 64, lane, sel4);
+    }
+    int half = 0;
+    for (int k = 128; k <= 1024; k <<= 1) {
+        for (int j = k >> 1; j >= 64; j >>= 1) {
+            double *e = ex + 1024 * half;
+#pragma unroll
+            for (int q = 0; q < NV; ++q) e[2048 * q + i] = x[q];
+            __syncthreads();
+            half ^= 1;  // the next exchange writes the other half: no second barrier
+            const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+#pragma unroll
+            for (int q = 0; q < NV; ++q) {
+                const double y = e[2048 * q + (i ^ j)];
+                x[q] = keep_min ? (y < x[q] ? y : x[q]) : (y > x[q] ? y : x[q]);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NV; ++q) bitonic_wave_steps<32>(x[q], i, k, lane, sel4);
+    }
+}
+
+// Ascending sort of v[0, m) (m a power of two) by 1024 threads.  m <= 1024: one element per
+// thread, +inf padding to 1024, sort_regs_1024 with v itself as the exchange (v must hold
+// 2048 elements).  Larger m: bitonic_sort_lds.
 __device__ void sort_1024(double *v, int m)
 {
     if (m > 1024) {
@@ -1394,26 +1481,11 @@ __device__ void sort_1024(double *v, int m)
         return;
     }
     const int i = threadIdx.x;
-    double x = i < m ? v[i] : INFINITY;
+    double x[1] = {i < m ? v[i] : INFINITY};
     __syncthreads();  // every thread has its element before v is reused as the exchange
-    int half = 0;
-    for (int k = 2; k <= 1024; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            double y;
-            if (j >= 64) {
-                double *ex = v + 1024 * half;
-                ex[i] = x;
-                __syncthreads();
-                y = ex[i ^ j];
-                half ^= 1;  // the next exchange writes the other half: no second barrier
-            } else {
-                y = __shfl_xor(x, j, 64);
-            }
-            const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
-            x = keep_min ? (y < x ? y : x) : (y > x ? y : x);
-        }
+    sort_regs_1024<1>(x, v);
     __syncthreads();  // every exchange read is done
-    if (i < m) v[i] = x;
+    if (i < m) v[i] = x[0];
     __syncthreads();
 }
 
@@ -1555,6 +1627,111 @@ variability_cert_kernel(const T *__restrict__ means, const double *__restrict__ 
     }
     const int any_unsure = __syncthreads_or(unsure);
     if (tid == 0) flag[0] = any_unsure ? 1 : 0;
+}
+
+// get_noisier_channels' decision and then measure_channel_variability's for that mask, in
+// ONE workgroup and one launch (n <= 1024; round 5: the two kernels above back to back).
+// Thread i owns channel i: the noisy-channel steps of noisy_channels_kernel (the two sorts
+// of the differences, the 7-window rank), the mask kept in a register as the variability
+// certification's bad mask (variability_cert_kernel's steps, the channel's std bounds
+// computed once, the lower- and upper-bound sorts sharing their barriers).  spec = the
+// row means (numpy's mean dtype T), mom their shifted moments (pu_row_moments).
+constexpr int kMasksMax = 1024;
+
+template <typename T>
+__global__ void __launch_bounds__(1024)
+channel_masks_kernel(const T *__restrict__ spec, const double *__restrict__ mom, int n, double c, double nd,
+                     double mef, double gam, double u, uint8_t *__restrict__ nmask, int32_t *__restrict__ nflag,
+                     uint8_t *__restrict__ vmask, int32_t *__restrict__ vflag)
+{
+    __shared__ double ex[2 * 2048];
+    __shared__ T sp[kMasksMax];
+    __shared__ double ord[8];  // order statistics handed between threads
+    const int tid = threadIdx.x;
+    const bool in = tid < n;
+    const T sv = in ? spec[tid] : T(0);
+    if (in) sp[tid] = sv;
+    if (__syncthreads_or(in && !isfinite((double)sv))) {
+        if (tid == 0) {
+            nflag[0] = 1;  // the host decides both masks
+            vflag[0] = 1;
+        }
+        return;
+    }
+    // ---- noisy channels (clean.py:58-67; noisy_channels_kernel)
+    const int nd1 = n - 1;
+    const double d = tid < nd1 ? (double)T(sp[tid + 1] - sp[tid]) : INFINITY;
+    auto median_of_sorted = [&](double v) {  // numpy's median of the nd1 sorted values
+        if (nd1 & 1) {
+            if (tid == nd1 / 2) ord[0] = v;
+        } else {
+            if (tid == nd1 / 2 - 1) ord[0] = v;
+            if (tid == nd1 / 2) ord[1] = v;
+        }
+        __syncthreads();
+        const double r = (nd1 & 1) ? ord[0] : (ord[0] + ord[1]) / 2.0;
+        __syncthreads();  // ord read by every thread before its next use
+        return r;
+    };
+    double x1[1] = {d};
+    sort_regs_1024<1>(x1, ex);
+    const double med = median_of_sorted(x1[0]);  // (its barriers also free ex)
+    x1[0] = tid < nd1 ? fabs(d - med) / c : INFINITY;
+    sort_regs_1024<1>(x1, ex);
+    const double rm = median_of_sorted(x1[0]) / 1.4142135623730951;  // np.sqrt(2)
+    const double thr = 5.0 * rm;
+    bool bad = false;
+    if (in) {
+        T w[7];
+#pragma unroll
+        for (int j = 0; j < 7; ++j) {
+            const int k = tid + j - 3;
+            w[j] = (k >= 0 && k < n) ? sp[k] : T(0);
+        }
+#pragma unroll
+        for (int a = 1; a < 7; ++a)
+#pragma unroll
+            for (int b = a; b > 0; --b)
+                if (w[b] < w[b - 1]) {
+                    const T t = w[b];
+                    w[b] = w[b - 1];
+                    w[b - 1] = t;
+                }
+        bad = (double)sv > (double)w[3] + thr;
+        nmask[tid] = bad ? 1 : 0;
+    }
+    if (tid == 0) nflag[0] = 0;
+    // ---- variability (clean.py:114-133; variability_cert_kernel) with bad = the noisy mask
+    const double *mr = mom + 3 * (in ? tid : 0);
+    const bool nf = in && (!isfinite(mr[0]) || !isfinite(mr[1]) || !isfinite(mr[2]));
+    const int any_nf = __syncthreads_or(nf);
+    const int ngood = __syncthreads_count(in && !bad);
+    if (any_nf || n / 4 * 3 >= ngood) {
+        if (tid == 0) vflag[0] = 1;
+        return;
+    }
+    double sl = INFINITY, sh = INFINITY;
+    if (in) variability_bounds((double)sv, mr, nd, mef, gam, u, sl, sh);
+    double x2[2] = {in && !bad ? sl : INFINITY, in && !bad ? sh : INFINITY};
+    sort_regs_1024<2>(x2, ex);
+    const int k1 = n / 4, k2 = n / 2, k3 = n / 4 * 3;
+    if (tid == k1) { ord[2] = x2[0]; ord[3] = x2[1]; }
+    if (tid == k2) { ord[4] = x2[0]; ord[5] = x2[1]; }
+    if (tid == k3) { ord[6] = x2[0]; ord[7] = x2[1]; }
+    __syncthreads();
+    const double a1 = ord[2], b1 = ord[3], a2 = ord[4], b2 = ord[5], a3 = ord[6], b3 = ord[7];
+    const double r = 4.0 * u * (b2 + 2.0 * (b3 - a1)) + 1e-300;
+    const double low_lo = (2.0 * a1 - b2) - r, low_hi = (2.0 * b1 - a2) + r;
+    const double hi_lo = (2.0 * a3 - b2) - r, hi_hi = (2.0 * b3 - a2) + r;
+    int unsure = 0;
+    if (in) {
+        const bool below = sh < low_lo, above = sl > hi_hi;
+        const bool sure = (below || sl >= low_hi) && (above || sh <= hi_lo);
+        unsure = !bad && !sure;
+        vmask[tid] = (below || above || bad) ? 1 : 0;
+    }
+    const int any_unsure = __syncthreads_or(unsure);
+    if (tid == 0) vflag[0] = any_unsure ? 1 : 0;
 }
 
 __global__ void ratio_dev_kernel(const double *__restrict__ num, const double *__restrict__ x, int64_t n,
@@ -2050,6 +2227,26 @@ int pu_noisy_channels(const void *spec, int dtype, int64_t n, double mad_c, uint
         hipLaunchKernelGGL(noisy_channels_kernel<double>, dim3(1), dim3(1024), 0, pu::as_stream(stream),
                            reinterpret_cast<const double *>(spec), (int)n, mad_c, mask, flag);
     return pu::launch_check("noisy_channels_kernel");
+}
+
+int pu_channel_masks(const void *means, int dtype, const double *moments, int64_t nrows, int64_t n, double mad_c,
+                     double mef, double gam, double u, uint8_t *noisy, int32_t *noisy_flag, uint8_t *var,
+                     int32_t *var_flag, void *stream)
+{
+    PU_REQUIRE(means && moments && noisy && noisy_flag && var && var_flag, "pu_channel_masks: NULL pointer");
+    PU_REQUIRE(nrows >= 2 && nrows <= kMasksMax, "pu_channel_masks: nrows = %lld outside [2, %d]", (long long)nrows,
+               kMasksMax);
+    PU_REQUIRE(n >= 1, "pu_channel_masks: n must be positive");
+    PU_REQUIRE(dtype == PU_F32 || dtype == PU_F64, "pu_channel_masks: means must be float32 or float64");
+    if (dtype == PU_F32)
+        hipLaunchKernelGGL(channel_masks_kernel<float>, dim3(1), dim3(1024), 0, pu::as_stream(stream),
+                           reinterpret_cast<const float *>(means), moments, (int)nrows, mad_c, (double)n, mef, gam, u,
+                           noisy, noisy_flag, var, var_flag);
+    else
+        hipLaunchKernelGGL(channel_masks_kernel<double>, dim3(1), dim3(1024), 0, pu::as_stream(stream),
+                           reinterpret_cast<const double *>(means), moments, (int)nrows, mad_c, (double)n, mef, gam,
+                           u, noisy, noisy_flag, var, var_flag);
+    return pu::launch_check("channel_masks_kernel");
 }
 
 int pu_ratio_dev(const double *numerator, const double *x, int64_t n, double *out, void *stream)

@@ -55,6 +55,7 @@ SIGNATURES = {
     "pu_median": (_i32, [_vp, _i64, _vp, _vp, _sz, _vp]),
     "pu_noisy_channels": (_i32, [_vp, _i32, _i64, _f64, _vp, _vp, _vp]),
     "pu_variability_cert": (_i32, [_vp, _i32, _vp, _i64, _i64, _f64, _f64, _f64, _vp, _vp, _vp, _vp]),
+    "pu_channel_masks": (_i32, [_vp, _i32, _vp, _i64, _i64, _f64, _f64, _f64, _f64, _vp, _vp, _vp, _vp, _vp]),
     "pu_ratio_dev": (_i32, [_vp, _vp, _i64, _vp, _vp]),
     "pu_lc_factor_workspace_bytes": (_sz, [_i64]),
     "pu_lc_factor": (_i32, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _sz, _vp]),

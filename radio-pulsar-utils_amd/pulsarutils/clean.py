@@ -178,6 +178,7 @@ def _host(t):
 
 
 _NOISY_MAX = 4096  # pu_noisy_channels: one workgroup
+_MASKS_MAX = 1024  # pu_channel_masks: one thread per channel
 
 
 def get_noisier_channels(array):
@@ -187,7 +188,8 @@ def get_noisier_channels(array):
     comparison in numpy's dtypes and order) and only the mask comes back; a spec with
     NaN / inf, or more than 4096 channels, is decided on the host by numpy / scipy.
     In the same read-back: measure_channel_variability's decision for this mask
-    (pu_variability_cert, queued behind it), kept for the same unmodified tensor - the
+    (pu_variability_cert, queued behind it; up to 1024 channels both decisions are one
+    launch, pu_channel_masks), kept for the same unmodified tensor - the
     usual next call, measure_channel_variability(x, badchans_mask=<this mask>), then
     needs no GPU work and no synchronisation of its own."""
     import weakref
@@ -200,12 +202,21 @@ def get_noisier_channels(array):
         # [noisy mask | its flag | variability mask | its flag]
         res = t.empty(2 * (off + 4), dtype=t.uint8, device=spec_d.device)
         base = res.data_ptr()
-        _hip.check(_hip.lib().pu_noisy_channels(_hip.ptr(spec_d), _hip.dtype_code(spec_d.dtype), n, float(MAD_C),
-                                                base, base + off, _hip.stream_ptr()),
-                   "pu_noisy_channels")
-        # (when the noisy flag is set the mask is unwritten: the variability result is
-        # then discarded)
-        _launch_variability(x, res[:n], base + off + 4, base + 2 * off + 4)
+        if n <= _MASKS_MAX and hasattr(_hip.lib(), "pu_channel_masks"):  # (absent: an older A/B build)
+            # both decisions in one launch (pu_channel_masks)
+            means, mom = _cached_stats(x)
+            mef, gam, u = _variability_args(means, x.shape[1])
+            _hip.check(_hip.lib().pu_channel_masks(_hip.ptr(means), _hip.dtype_code(means.dtype), _hip.ptr(mom), n,
+                                                   x.shape[1], float(MAD_C), mef, gam, u, base, base + off,
+                                                   base + off + 4, base + 2 * off + 4, _hip.stream_ptr()),
+                       "pu_channel_masks")
+        else:
+            _hip.check(_hip.lib().pu_noisy_channels(_hip.ptr(spec_d), _hip.dtype_code(spec_d.dtype), n,
+                                                    float(MAD_C), base, base + off, _hip.stream_ptr()),
+                       "pu_noisy_channels")
+            # (when the noisy flag is set the mask is unwritten: the variability result is
+            # then discarded)
+            _launch_variability(x, res[:n], base + off + 4, base + 2 * off + 4)
         h = _host(res)
         if not h[off:off + 4].view(np.int32)[0]:
             mask = h[:n].astype(bool)

@@ -529,6 +529,57 @@ def test_variability_cert_device_matches_host(gpu, dtype, nchan, n):
                 np.testing.assert_array_equal(host, co.channel_variability(x, badchans_mask=bad))
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64, np.uint8])
+@pytest.mark.parametrize("nchan", [2, 3, 5, 8, 63, 64, 65, 500, 1023, 1024])
+def test_channel_masks_one_launch_matches_two_kernels(gpu, dtype, nchan):
+    """pu_channel_masks (round 5: both decisions in one workgroup) writes the same bytes as
+    pu_noisy_channels followed by pu_variability_cert with the noisy mask as bad - masks and
+    flags - on spectra with noisy channels, a channel at the variability limit region, and
+    a non-finite spectrum (both flags set)."""
+    from pulsarutils import _hip
+    import torch
+    rng = np.random.default_rng(7 * nchan + np.dtype(dtype).itemsize)
+    ns = 2048
+    for case in range(3):
+        x = rng.normal(100.0, 5.0, (nchan, ns)) * rng.uniform(0.7, 1.4, nchan)[:, None]
+        if case >= 1:
+            x[rng.random(nchan) < 0.1] += 40.0  # noisy channels
+        x = (np.clip(x, 0, 255) if dtype == np.uint8 else x).astype(dtype)
+        if case == 2 and dtype != np.uint8:
+            x[nchan // 2, 3] = np.nan
+        xd = _hip.to_device(x)
+        C.invalidate_channel_means()
+        means, mom = C._cached_stats(xd)
+        mef, gam, u = C._variability_args(means, ns)
+        off = (nchan + 3) & ~3
+        lib = _hip.lib()
+        one = torch.full((2 * (off + 4),), 7, dtype=torch.uint8, device=xd.device)
+        b = one.data_ptr()
+        _hip.check(lib.pu_channel_masks(_hip.ptr(means), _hip.dtype_code(means.dtype), _hip.ptr(mom), nchan, ns,
+                                        float(C.MAD_C), mef, gam, u, b, b + off, b + off + 4, b + 2 * off + 4,
+                                        _hip.stream_ptr()), "pu_channel_masks")
+        two = torch.full((2 * (off + 4),), 7, dtype=torch.uint8, device=xd.device)
+        b = two.data_ptr()
+        _hip.check(lib.pu_noisy_channels(_hip.ptr(means), _hip.dtype_code(means.dtype), nchan, float(C.MAD_C), b,
+                                         b + off, _hip.stream_ptr()), "pu_noisy_channels")
+        h1, h2 = one.cpu().numpy(), two.cpu().numpy()
+        nflag = int(h2[off:off + 4].view(np.int32)[0])
+        assert int(h1[off:off + 4].view(np.int32)[0]) == nflag
+        if nflag:
+            assert case == 2 and dtype != np.uint8
+            assert int(h1[2 * off + 4:2 * off + 8].view(np.int32)[0]) == 1
+            continue
+        np.testing.assert_array_equal(h1[:nchan], h2[:nchan])
+        _hip.check(lib.pu_variability_cert(_hip.ptr(means), _hip.dtype_code(means.dtype), _hip.ptr(mom), nchan, ns,
+                                           mef, gam, u, b, b + off + 4, b + 2 * off + 4, _hip.stream_ptr()),
+                   "pu_variability_cert")
+        h2 = two.cpu().numpy()
+        vflag = int(h2[2 * off + 4:2 * off + 8].view(np.int32)[0])
+        assert int(h1[2 * off + 4:2 * off + 8].view(np.int32)[0]) == vflag
+        if not vflag:
+            np.testing.assert_array_equal(h1[off + 4:off + 4 + nchan], h2[off + 4:off + 4 + nchan])
+
+
 @pytest.mark.parametrize("dt", ["f32", "u8"])
 def test_masks_one_readback_on_device_tensor(gpu, golden, dt):
     """get_noisier_channels on a device tensor also decides measure_channel_variability
