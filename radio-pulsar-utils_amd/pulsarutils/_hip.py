@@ -168,19 +168,27 @@ def torch():
     return _t
 
 
+_GPU_OK = [False]
+
+
 def require_gpu():
     t = torch()
-    if not t.cuda.is_available():
-        raise HipBackendError("pulsarutils: the dedispersion/cleaning path runs on a ROCm GPU "
-                              "(MI355X / gfx950); torch.cuda.is_available() is False")
-    lib()
+    if not _GPU_OK[0]:  # (checked once: is_available() costs a few microseconds per call)
+        if not t.cuda.is_available():
+            raise HipBackendError("pulsarutils: the dedispersion/cleaning path runs on a ROCm GPU "
+                                  "(MI355X / gfx950); torch.cuda.is_available() is False")
+        lib()
+        _GPU_OK[0] = True
     return t
 
 
 def stream_ptr(stream=None):
+    """The hipStream_t of ``stream``, or of torch's current stream on the current device -
+    read raw (no Stream object: torch.cuda.current_stream() costs ~3 us per call)."""
+    if stream is not None:
+        return ctypes.c_void_p(stream.cuda_stream)
     t = torch()
-    s = stream if stream is not None else t.cuda.current_stream()
-    return ctypes.c_void_p(s.cuda_stream)
+    return ctypes.c_void_p(t._C._cuda_getCurrentRawStream(t.cuda.current_device()))
 
 
 def ptr(tensor):

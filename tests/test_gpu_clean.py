@@ -652,3 +652,16 @@ def test_light_curve_factor(gpu, n, sigma):
         _hip.check(lib.pu_ratio_dev(_hip.ptr(C.median_device(sm)), _hip.ptr(sm), n, _hip.ptr(f3), _hip.stream_ptr()),
                    "pu_ratio_dev")
         assert torch.equal(f3.isnan(), got.isnan()) and torch.equal(f3.nan_to_num(), got.nan_to_num())
+
+
+def test_stream_ptr_is_torch_current_stream(gpu):
+    """_hip.stream_ptr() (read raw, round 5) is torch's current stream, also inside a
+    ``torch.cuda.stream`` block, and an explicit stream's own handle (the null stream: a NULL pointer, c_void_p(0).value is None)."""
+    from pulsarutils import _hip
+    import torch
+    assert (_hip.stream_ptr().value or 0) == torch.cuda.current_stream().cuda_stream
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        assert (_hip.stream_ptr().value or 0) == s.cuda_stream
+    assert (_hip.stream_ptr(s).value or 0) == s.cuda_stream
+    assert (_hip.stream_ptr().value or 0) == torch.cuda.current_stream().cuda_stream
