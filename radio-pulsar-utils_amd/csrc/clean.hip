@@ -1416,13 +1416,35 @@ __device__ __forceinline__ double lane_xor(double x, int lane, bool sel4)
     return __builtin_bit_cast(double, (uint64_t)w[0] | ((uint64_t)w[1] << 32));
 }
 
+// min / max of two doubles that are never NaN (finite or +inf: the sorts' callers check) in
+// one instruction each (a compare + two selects per 32-bit half otherwise)
+__device__ __forceinline__ double min_nn(double a, double b)
+{
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double max_nn(double a, double b)
+{
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+// the bitonic compare-exchange of x with its partner y: the smaller value stays when
+// keep_min (exact: min / max of non-NaN values)
+__device__ __forceinline__ double bitonic_keep(double x, double y, bool keep_min)
+{
+    const double lo = min_nn(x, y), hi = max_nn(x, y);
+    return keep_min ? lo : hi;
+}
+
 // the in-wave bitonic steps j = J, J/2, .., 1 of merge size k (lane_xor exchanges)
 template <int J>
 __device__ __forceinline__ void bitonic_wave_steps(double &x, int i, int k, int lane, bool sel4)
 {
     const double y = lane_xor<J>(x, lane, sel4);
-    const bool keep_min = ((i & J) == 0) == ((i & k) == 0);
-    x = keep_min ? (y < x ? y : x) : (y > x ? y : x);
+    x = bitonic_keep(x, y, ((i & J) == 0) == ((i & k) == 0));
     if constexpr (J > 1) bitonic_wave_steps<J / 2>(x, i, k, lane, sel4);
 }
 
@@ -1461,10 +1483,7 @@ __device__ void sort_regs_1024(double (&x)[NV], double *ex)
             half ^= 1;  // the next exchange writes the other half: no second barrier
             const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
 #pragma unroll
-            for (int q = 0; q < NV; ++q) {
-                const double y = e[2048 * q + (i ^ j)];
-                x[q] = keep_min ? (y < x[q] ? y : x[q]) : (y > x[q] ? y : x[q]);
-            }
+            for (int q = 0; q < NV; ++q) x[q] = bitonic_keep(x[q], e[2048 * q + (i ^ j)], keep_min);
         }
 #pragma unroll
         for (int q = 0; q < NV; ++q) bitonic_wave_steps<32>(x[q], i, k, lane, sel4);
