@@ -279,6 +279,7 @@ __global__ void rowsum_combine(const Ta *__restrict__ block_sums, int64_t nrows,
     const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (row >= nrows) return;
     Ta acc = Ta(0);
+#pragma unroll 8
     for (int64_t k = 0; k < nblk_row; ++k) acc += block_sums[row * nblk_row + k];
     if (divisor > 0) acc = static_cast<Ta>(static_cast<double>(acc) / divisor);
     out[row] = acc;

@@ -370,6 +370,27 @@ def light_curve_factor(lc, weights, radius, median_out=None):
     return factor
 
 
+_MASK = {}  # (device, stream) -> (mask bytes, the device copy): the last uploaded channel mask
+
+
+def _device_mask(bad_np, dev):
+    """The uint8 channel mask ``bad_np`` on ``dev``: the previous call's copy when the bytes
+    are the same (read-only in the kernels; a new tensor otherwise, so a copy still in use
+    by queued work is never overwritten; per stream, so the copy is ordered before every
+    reader).  The upload goes through pinned memory
+    asynchronously: a pageable copy would block the host until the stream drained (the
+    previous call's kernels), so the next call's launches could not queue behind them."""
+    key = bad_np.tobytes()
+    slot = (str(dev), _hip.stream_ptr().value)
+    c = _MASK.get(slot)
+    if c is not None and c[0] == key:
+        return c[1]
+    t = _hip.torch()
+    bad = t.from_numpy(bad_np).pin_memory().to(dev, non_blocking=True)
+    _MASK[slot] = (key, bad)
+    return bad
+
+
 def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=False, out=None,
                        zero_dm=False):
     """renormalize_data on a device tensor; returns (float64 device tensor, bad_bins or None),
@@ -397,10 +418,7 @@ def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=
     if badchans_mask is None:
         badchans_mask = np.zeros(nchan, dtype=bool)
     bad_np = np.ascontiguousarray(np.asarray(badchans_mask, dtype=bool)).astype(np.uint8)
-    # the mask goes through pinned memory asynchronously: a pageable copy would block
-    # the host until the stream drained (the previous call's kernels), so the next
-    # call's launches could not queue behind them
-    bad = t.from_numpy(bad_np).pin_memory().to(dev, non_blocking=True)
+    bad = _device_mask(bad_np, dev)
     sigma = min(baseline_window, n // 100 * 2 + 1)
     dw, radius = _gaussian_weights_device(sigma, dev)
     lc = t.empty(n, dtype=t.float64, device=dev)
