@@ -356,7 +356,7 @@ def main():
     ap.add_argument("--ref-steps", type=int, default=1)
     ap.add_argument("--cpu-trials", type=int, default=400)
     ap.add_argument("--no-clean", action="store_true")
-    ap.add_argument("--clean-steps", type=int, default=5)
+    ap.add_argument("--clean-steps", type=int, default=20)
     ap.add_argument("--bcast-chunks", type=int, default=8)
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--no-c3-strong", action="store_true",
