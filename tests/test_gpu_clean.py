@@ -80,6 +80,33 @@ def test_renormalize_api_matches_oracle_small(gpu):
     np.testing.assert_array_equal(C.renormalize_data(x), co.renormalize(x))
 
 
+def test_renormalize_channel_mask_reuse(gpu):
+    """renormalize_device reuses the device copy of an unchanged channel mask (round 5):
+    alternating masks A, B, A, an all-false mask (None) and A again, also on a second
+    stream, each equal to the numpy restatement - a changed mask is never served stale."""
+    import torch
+    from pulsarutils import _hip
+    rng = np.random.default_rng(21)
+    x = (rng.random((24, 900)) * 5 + 1).astype(np.float32)
+    xd = _hip.to_device(x)
+    a = np.zeros(24, bool)
+    a[[1, 5]] = True
+    b = np.zeros(24, bool)
+    b[[5, 17, 20]] = True
+    s2 = torch.cuda.Stream()
+    for i, m in enumerate([a, b, a, None, a, b]):
+        def run():
+            out, _ = C.renormalize_device(xd, badchans_mask=m, cut_outliers=True)
+            return out.cpu().numpy()
+        if i >= 4:
+            s2.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s2):
+                got = run()
+        else:
+            got = run()
+        np.testing.assert_array_equal(got, co.renormalize(x, badchans_mask=m, cut_outliers=True))
+
+
 @pytest.mark.parametrize("dt", ["f32", "u8", "f64"])
 @pytest.mark.parametrize("n,pad,off", [(12346, 6, 0), (16388, 4, 2), (8192 * 2 + 8, 0, 1)])
 def test_clean_strided_views(gpu, dt, n, pad, off):
