@@ -16,6 +16,9 @@ from garbage.  Checks (bit for bit):
     _dedispersion_search of each rank's trial slice (the same plans);
   * CASE C5m: the same with reserve_cus=8 (the CU-masked compute stream), outputs freed
     afterwards (the masked stream must outlive the tensors recorded on it).
+MR_BACKEND=nccl (environment): an RCCL process group instead (WORLD 1 on the one GPU: the
+RCCL calls of the product path - broadcast on the communication stream, all_gather,
+barrier - with a single rank).
 COLLECTIVE (default broadcast): the chunk exchange of parallel.exchange_chunk -
 ``broadcast`` or ``scatter_allgather`` (the mesh variant, round 5).
 Prints ``RANK r OK`` and exits 0, or raises (non-zero exit, traceback on stderr).
@@ -42,7 +45,12 @@ def main():
     from pulsarutils.configs import CONFIGS
 
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    backend = os.environ.get("MR_BACKEND", "gloo")  # nccl (RCCL): one rank per GPU only
+    if backend == "nccl":
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     src = world - 1
     c, ntrials, chunks, reserve = {
         "C5": (CONFIGS["C5"], 500, 5, 0),
@@ -92,7 +100,7 @@ def main():
     assert ntrials < full.size or abs(dms[best] - c.pulse_dm) < 1.0, (dms[best], c.pulse_dm)
     dist.barrier()
     dist.destroy_process_group()
-    print(f"RANK {rank} OK case {case} world {world} {collective} best DM {dms[best]:.3f} snr {snr[best]:.3f}", flush=True)
+    print(f"RANK {rank} OK case {case} world {world} {backend} {collective} best DM {dms[best]:.3f} snr {snr[best]:.3f}", flush=True)
 
 
 if __name__ == "__main__":

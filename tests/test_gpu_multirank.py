@@ -50,3 +50,16 @@ def test_multirank_pipelined_and_sharded_on_one_gpu(gpu, world, case, collective
     for r, (rc, o, e) in enumerate(outs):
         assert rc == 0 and f"RANK {r} OK" in o, f"rank {r} rc {rc}\n{o}\n{e[-4000:]}"
     print("\n".join(o.strip() for _, o, _ in outs))
+
+
+@pytest.mark.parametrize("case,collective", [("C5", "broadcast"), ("C3s", "scatter_allgather")])
+def test_rccl_process_group_one_rank(gpu, case, collective):
+    """The product path's collectives on an RCCL ("nccl") process group: one rank on the one
+    GPU (RCCL takes one rank per device), so the same worker's broadcast / all_gather /
+    barrier run through RCCL itself, bit-equal to the single-process search."""
+    port = _free_port()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="4", MR_BACKEND="nccl")
+    p = subprocess.run([sys.executable, "-u", os.path.join(HERE, "mr_worker.py"), "0", "1", str(port), case,
+                        collective], capture_output=True, timeout=240, env=env)
+    o, e = p.stdout.decode(errors="replace"), p.stderr.decode(errors="replace")
+    assert p.returncode == 0 and "RANK 0 OK" in o and " nccl " in o, f"rc {p.returncode}\n{o}\n{e[-4000:]}"
