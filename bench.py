@@ -212,7 +212,7 @@ def acc_f64_bench(x, dms, cfg, steps):
     info = plan.info
     lds = info["lds_traffic"] / (kms / 1e3) / 1e12
     res = {"workload": f"{cfg.name} ({dms.size} trials), float64 accumulation in channel order (acc='f64')",
-           "kernel": "dedisp_kernel", "steps": steps, "ms_per_step": round(step_ms, 4), "kernel_ms": round(kms, 4),
+           "kernel": _hip.KERNEL_NAMES[info["kernel"]], "steps": steps, "ms_per_step": round(step_ms, 4), "kernel_ms": round(kms, 4),
            "value": dms.size * cfg.nsamples / (step_ms / 1e3), "unit": "DM-trial samples/s",
            "roofline": {"bound": "valu", "achieved": round(adds / (kms / 1e3) / 1e12, 3),
                         "peak": VALU_F64_ADD_PEAK_TFLOPS, "unit": "TFLOP/s (f64 adds)",
@@ -442,17 +442,21 @@ def main():
         if rank == 0:
             log(f"exchange {bcast}")
 
-    def step():
+    def step(phases=None):
         if pipelined:
             # the whole job: rank 0's filterbank distributed in time chunks, every rank
             # searching the tiles whose rows have landed, then the finalize
             pipelined_broadcast_search(x, plan, outs, ws, src=0, chunks=args.bcast_chunks,
-                                       collective=args.collective)
+                                       collective=args.collective, phases=phases)
         else:
             plan.search(x, out=outs, workspace=ws)
         if world > 1:
+            if phases is not None:
+                phases.mark("gather", torch.cuda.current_stream(dev))
             local_stats[:, :per_rank].copy_(torch.stack([outs[0], outs[1], outs[2], outs[3].to(torch.float64)]))
             dist.all_gather_into_tensor(gathered, local_stats)
+            if phases is not None:
+                phases.mark("gather", torch.cuda.current_stream(dev), end=True)
 
     for i in range(args.warmup):
         step()
@@ -477,6 +481,28 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     ms_per_step = elapsed / args.steps * 1e3
+
+    # N > 1, pipelined: one more (untimed) step with HIP events around its phases - the
+    # exchange, unpack and tile searches per chunk, the finalize, the gather - so a scaling
+    # run explains itself; per phase the max over ranks
+    phase_ms = None
+    if pipelined:
+        from pulsarutils.parallel import PhaseEvents
+        pe = PhaseEvents()
+        dist.barrier()
+        step(pe)
+        torch.cuda.synchronize()
+        mine = pe.times_ms()
+        keys = sorted(k for k, v in mine.items() if not isinstance(v, list))
+        vals = torch.tensor([float(mine[k]) for k in keys], dtype=torch.float64, device=dev)
+        allv = torch.empty(world * len(keys), dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(allv, vals)
+        allv = allv.view(world, len(keys)).cpu().numpy()
+        phase_ms = {"what": "one extra untimed step with HIP events: per-chunk exchange (scatter + all-gather "
+                            "or broadcast) and unpack (staging -> strided column chunk, receivers) on the "
+                            "communication stream, tile searches per chunk, finalize, gather; exposed_tail = "
+                            "last chunk landed -> finalize done",
+                    "rank0": mine, "max_over_ranks": {k: round(float(allv[:, i].max()), 4) for i, k in enumerate(keys)}}
 
     # spot check: best trial of the whole grid (rank 0's view of the gathered S/N)
     if world > 1:
@@ -507,7 +533,7 @@ def main():
         roof = {"bound": "valu", "achieved": round(achieved, 3), "peak": peak,
                 "unit": "TFLOP/s" + (" (f64 adds)" if acc64 else " (f32 adds)"),
                 "frac": round(achieved / peak, 4), "traffic": traffic,
-                "kernel": "dedisp_sub_kernel" if info["group"] > 1 else "dedisp_kernel",
+                "kernel": _hip.KERNEL_NAMES[info["kernel"]],
                 "kernel_ms": round(kernel_ms, 4),
                 "algorithmic_flop_per_launch": adds, "algorithmic_bytes_per_launch": alg_bytes,
                 "time_tiles": info["time_tiles"],
@@ -622,6 +648,8 @@ def main():
             line["multi_gpu"] = bcast
         if ref1 is not None:
             line["single_gpu_same_workload"] = ref1
+        if phase_ms is not None:
+            line["phases"] = phase_ms
         line["build"] = _hip.build_info()  # was the library built from the sources shipped with it
         print(json.dumps(line), flush=True)
     if world > 1:

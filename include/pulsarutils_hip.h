@@ -175,11 +175,13 @@ int pu_plan_stamps(pu_plan *plan, int64_t *out, int n);
  * {ndm, dm_tiles, time_tiles, trials_per_tile, time_tile, chans_per_step,
  *  row_stride, lds_bytes, acc_is_f64, max_spread, group, slots, stages,
  *  slot_bytes, raw_stride, exec_adds, lds_traffic, cert_rechecked, cert_nan, cert_std,
- *  cert_sign, cert_tie, cert_us}: exec_adds and lds_traffic are the adds and LDS bytes (reads,
+ *  cert_sign, cert_tie, cert_us, kernel}: exec_adds and lds_traffic are the adds and LDS bytes (reads,
  *  writes, DMA) one launch executes (subband mode; 0 otherwise); the cert_* fields
  *  describe the last search's certification step (see pu_plan_finalize): trials
  *  recomputed, the NaN rule, and how many trials each check flagged (std not above its
- *  rounding bound, S/N sign, S/N tie) and the host microseconds spent settling them.
+ *  rounding bound, S/N sign, S/N tie) and the host microseconds spent settling them;
+ *  kernel: 0 dedisp_kernel (channel order), 1 dedisp_f64_kernel, 2 dedisp_sub_kernel
+ *  (float32 slots), 3 dedisp_sub_kernel with 16-bit integer slots (8-bit input).
  *  Returns the count written. */
 int pu_plan_info(const pu_plan *plan, int64_t *info, int n);
 

@@ -41,6 +41,8 @@ def lib():
         L.or_dedisperse.restype = None
         L.or_search.argtypes = [vp, ctypes.c_int, i64, i64, i64, vp, i64, f64, f64, f64,
                                 vp, vp, vp, vp, vp, ctypes.c_int]
+        L.or_search_w.argtypes = [vp, ctypes.c_int, i64, i64, i64, vp, i64, f64, f64, f64,
+                                  vp, vp, vp, vp, vp, vp, ctypes.c_int]
         L.or_np_sum.argtypes = [vp, i64]
         L.or_np_sum.restype = f64
         L.or_np_std.argtypes = [vp, i64, vp]
@@ -73,9 +75,14 @@ def dedisperse(data, shifts_):
     return out
 
 
-def search(data, trial_dms, start_freq, bandwidth, sample_time, nthreads=0, return_dedisp=False):
-    """``_dedispersion_search`` restated: returns (max, std, snr, rebin[int32])."""
-    data = np.ascontiguousarray(data)
+def search(data, trial_dms, start_freq, bandwidth, sample_time, nthreads=0, return_dedisp=False,
+           return_width_snr=False):
+    """``_dedispersion_search`` restated: returns (max, std, snr, rebin[int32]), then the
+    dedispersed series ``[ndm, n]`` if ``return_dedisp``, then (test-side only) the S/N of
+    each rebin width 1/2/4/8 ``[ndm, 4]`` if ``return_width_snr`` (the candidates of the
+    reference's first-strict-best choice, ``dedispersion.py:189-201``; NaN for widths longer
+    than the series)."""
+    data =np.ascontiguousarray(data)
     if data.dtype not in _DT:
         data = data.astype(np.float64)
     dms = np.ascontiguousarray(trial_dms, dtype=np.float64)
@@ -84,13 +91,19 @@ def search(data, trial_dms, start_freq, bandwidth, sample_time, nthreads=0, retu
     mx, sd, snr = (np.empty(nd) for _ in range(3))
     win = np.empty(nd, np.int64)
     dd = np.empty((nd, n)) if return_dedisp else None
-    rc = lib().or_search(_p(data), _DT[data.dtype], nchan, n, n, _p(dms), nd, float(start_freq),
-                         float(bandwidth), float(sample_time), _p(mx), _p(sd), _p(snr), _p(win),
-                         _p(dd) if dd is not None else None, int(nthreads))
+    sw = np.full((nd, 4), np.nan) if return_width_snr else None
+    rc = lib().or_search_w(_p(data), _DT[data.dtype], nchan, n, n, _p(dms), nd, float(start_freq),
+                           float(bandwidth), float(sample_time), _p(mx), _p(sd), _p(snr), _p(win),
+                           _p(dd) if dd is not None else None, _p(sw) if sw is not None else None,
+                           int(nthreads))
     if rc:
         raise MemoryError("oracle search failed")
     out = (mx, sd, snr, win.astype(np.int32))
-    return out + (dd,) if return_dedisp else out
+    if return_dedisp:
+        out = out + (dd,)
+    if return_width_snr:
+        out = out + (sw,)
+    return out
 
 
 def trial_stats(dedisp):

@@ -150,8 +150,8 @@ double or_np_std(const double *a, int64_t n, double *scratch)
 
 /* One trial of _dedispersion_search (dedispersion.py:182-201) on a dedispersed
  * series ``dd`` (n doubles).  work: 2n doubles. */
-void or_trial_stats(const double *dd, int64_t n, double *work, double *max_out,
-                    double *std_out, double *snr_out, int64_t *win_out)
+static void trial_stats_w(const double *dd, int64_t n, double *work, double *max_out,
+                          double *std_out, double *snr_out, int64_t *win_out, double *snr_w)
 {
     double *shifted = work, *reb = work + n;
     double mean = or_np_sum(dd, n) / (double)n;
@@ -181,6 +181,7 @@ void or_trial_stats(const double *dd, int64_t n, double *work, double *max_out,
         double sd = sqrt(or_np_sum(sq, nb) / (double)nb);
         free(sq);
         double snr = mx / sd;
+        if (snr_w) snr_w[wp] = snr;
         if (snr > best_snr) {
             best_snr = snr;
             best_win = w;
@@ -201,12 +202,20 @@ void or_trial_stats(const double *dd, int64_t n, double *work, double *max_out,
     *win_out = best_win;
 }
 
+void or_trial_stats(const double *dd, int64_t n, double *work, double *max_out,
+                    double *std_out, double *snr_out, int64_t *win_out)
+{
+    trial_stats_w(dd, n, work, max_out, std_out, snr_out, win_out, NULL);
+}
+
 /* _dedispersion_search: trials in parallel (numba prange -> OpenMP).
- * dedisp_out (nullable): [ndm][n] float64 dedispersed series. */
-int or_search(const void *data, int dtype, int64_t nchan, int64_t n, int64_t ld,
-              const double *dms, int64_t ndm, double start_freq, double bandwidth,
-              double sample_time, double *max_out, double *std_out, double *snr_out,
-              int64_t *win_out, double *dedisp_out, int nthreads)
+ * dedisp_out (nullable): [ndm][n] float64 dedispersed series.
+ * snr_w_out (nullable, test-side only): [ndm][4] the S/N of each rebin width 1/2/4/8
+ * (entries of widths longer than the series are left as they are). */
+int or_search_w(const void *data, int dtype, int64_t nchan, int64_t n, int64_t ld,
+                const double *dms, int64_t ndm, double start_freq, double bandwidth,
+                double sample_time, double *max_out, double *std_out, double *snr_out,
+                int64_t *win_out, double *dedisp_out, double *snr_w_out, int nthreads)
 {
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
@@ -225,13 +234,23 @@ int or_search(const void *data, int dtype, int64_t nchan, int64_t n, int64_t ld,
                 or_shifts(nchan, dms[i], start_freq, bandwidth, sample_time, sh);
                 or_dedisperse(data, dtype, nchan, n, ld, sh, dd);
                 if (dedisp_out) memcpy(dedisp_out + (size_t)i * (size_t)n, dd, sizeof(double) * (size_t)n);
-                or_trial_stats(dd, n, dd + n, &max_out[i], &std_out[i], &snr_out[i], &win_out[i]);
+                trial_stats_w(dd, n, dd + n, &max_out[i], &std_out[i], &snr_out[i], &win_out[i],
+                              snr_w_out ? snr_w_out + 4 * i : NULL);
             }
         }
         free(dd);
         free(sh);
     }
     return err ? -1 : 0;
+}
+
+int or_search(const void *data, int dtype, int64_t nchan, int64_t n, int64_t ld,
+              const double *dms, int64_t ndm, double start_freq, double bandwidth,
+              double sample_time, double *max_out, double *std_out, double *snr_out,
+              int64_t *win_out, double *dedisp_out, int nthreads)
+{
+    return or_search_w(data, dtype, nchan, n, ld, dms, ndm, start_freq, bandwidth, sample_time, max_out,
+                       std_out, snr_out, win_out, dedisp_out, NULL, nthreads);
 }
 
 int or_max_threads(void)

@@ -25,6 +25,7 @@
 //                        an LDS window (gauss_kernel: direct form for huge radii).
 //   apply_kernel         (x*f - mu)/mu, bad rows zeroed, optional column mean (:81-94),
 //                        V adjacent columns per lane.
+#include <atomic>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -1458,7 +1459,7 @@ __device__ __forceinline__ double lane_xor(double x, int lane, bool sel4)
     return __builtin_bit_cast(double, (uint64_t)w[0] | ((uint64_t)w[1] << 32));
 }
 
-// min / max of two doubles that are never NaN (finite or +inf: the sorts' callers check) in
+// min / max of two doubles that are never NaN (the sorts' callers check: __syncthreads_or) in
 // one instruction each (a compare + two selects per 32-bit half otherwise)
 __device__ __forceinline__ double min_nn(double a, double b)
 {
@@ -1496,8 +1497,8 @@ __device__ __forceinline__ void bitonic_wave_steps(double &x, int i, int k, int 
 // exchange on the VALU (lane_xor: DPP and permlane swaps, no barrier; round 5 first:
 // __shfl_xor, an LDS permute per step), the 10 with a partner in another wave through ex
 // (NV x 2048 doubles of LDS, two alternating halves per sort: one barrier per step).  ex
-// must be free on entry; the caller synchronises before reusing it.  The values are finite
-// or +inf (the callers check), so min / max by comparison are exact.
+// must be free on entry; the caller synchronises before reusing it.  No value is NaN (each
+// caller tests that first and hands the decision to the host), so min / max are exact.
 template <int NV>
 __device__ void sort_regs_1024(double (&x)[NV], double *ex)
 {
@@ -1584,9 +1585,17 @@ noisy_channels_kernel(const T *__restrict__ spec, int n, double c, uint8_t *__re
     sort_1024(ev, m);
     const double med = median_sorted(ev, n - 1);
     __syncthreads();  // every thread has read the median before ev is overwritten
-    for (int i = tid; i < m; i += 1024)
+    int nan_e = 0;
+    for (int i = tid; i < m; i += 1024) {
         ev[i] = i < n - 1 ? fabs((double)T(sp[i + 1] - sp[i]) - med) / c : INFINITY;
-    __syncthreads();
+        nan_e |= isnan(ev[i]);
+    }
+    // a NaN (inf - inf after a float32 difference overflowed) would be dropped by the
+    // register sort's min / max: the host decides
+    if (__syncthreads_or(nan_e)) {
+        if (tid == 0) flag[0] = 1;
+        return;
+    }
     sort_1024(ev, m);
     const double rm = median_sorted(ev, n - 1) / 1.4142135623730951;  // np.sqrt(2)
     const double thr = 5.0 * rm;
@@ -1738,6 +1747,15 @@ channel_masks_kernel(const T *__restrict__ spec, const double *__restrict__ mom,
     sort_regs_1024<1>(x1, ex);
     const double med = median_of_sorted(x1[0]);  // (its barriers also free ex)
     x1[0] = tid < nd1 ? fabs(d - med) / c : INFINITY;
+    // the register sorts' v_min_f64 / v_max_f64 drop a NaN operand: a NaN here (a float32
+    // difference that overflowed to inf, then inf - inf) hands both decisions to the host
+    if (__syncthreads_or(isnan(x1[0]))) {
+        if (tid == 0) {
+            nflag[0] = 1;
+            vflag[0] = 1;
+        }
+        return;
+    }
     sort_regs_1024<1>(x1, ex);
     const double rm = median_of_sorted(x1[0]) / 1.4142135623730951;  // np.sqrt(2)
     const double thr = 5.0 * rm;
@@ -1774,6 +1792,10 @@ channel_masks_kernel(const T *__restrict__ spec, const double *__restrict__ mom,
     double sl = INFINITY, sh = INFINITY;
     if (in) variability_bounds((double)sv, mr, nd, mef, gam, u, sl, sh);
     double x2[2] = {in && !bad ? sl : INFINITY, in && !bad ? sh : INFINITY};
+    if (__syncthreads_or(isnan(x2[0]) || isnan(x2[1]))) {  // (NaN bounds: the host decides)
+        if (tid == 0) vflag[0] = 1;
+        return;
+    }
     sort_regs_1024<2>(x2, ex);
     const int k1 = n / 4, k2 = n / 2, k3 = n / 4 * 3;
     if (tid == k1) { ord[2] = x2[0]; ord[3] = x2[1]; }
@@ -2169,6 +2191,31 @@ size_t pu_cut_outliers_workspace_bytes(int64_t n)
 }
 
 namespace {
+// CUs a launch on stream s may use: the current device's, or the stream's CU mask's when it
+// has one (pu_stream_create_cu_masked); 0 if they cannot be counted.
+int usable_cus(hipStream_t s)
+{
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    static std::atomic<int> ncu[64];
+    cus = dev < 64 ? ncu[dev].load() : 0;
+    if (cus <= 0) {
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+        if (dev < 64) ncu[dev].store(cus);
+    }
+    if (s) {
+        uint32_t m[32] = {};
+        if (hipExtStreamGetCUMask(s, 32, m) == hipSuccess) {
+            int c = 0;
+            for (uint32_t w : m) c += __builtin_popcount(w);
+            if (c > 0 && c < cus) cus = c;
+        } else {
+            (void)hipGetLastError();
+        }
+    }
+    return cus;
+}
+
 int cut_outliers(const double *lc, int64_t n, double *out, int64_t nrows, int64_t ld_out, uint8_t *mask, void *ws,
                  size_t ws_bytes, void *stream, bool exact_only)
 {
@@ -2184,21 +2231,40 @@ int cut_outliers(const double *lc, int64_t n, double *out, int64_t nrows, int64_
     // one 16-byte-multiple fill (the runtime splits a 56-byte memset into two kernels)
     static_assert(sizeof(OutlierState) <= 64, "OutlierState fits the cleared 64 bytes");
     static_assert(sizeof(OutlierBar) <= 64, "OutlierBar fits the cleared 64 bytes after the state");
+    bool resident = false;
     if (!exact_only) {
         // one launch with grid barriers (outlier_fused_kernel): at most one workgroup per two
-        // CUs, each with <= 64 KB of window means in LDS, so the whole grid is resident
-        static int cus = 0;
-        if (!cus) PU_TRY_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+        // CUs the stream may use, each with <= 64 KB of window means in LDS, and never more
+        // than the occupancy calculator says can be resident on them together - so every
+        // workgroup of the grid is resident and the spinning barrier cannot wait on one that
+        // never starts.  Counted per call on the current device and the stream's CU mask (a
+        // CU-masked stream, pu_stream_create_cu_masked, sees only its CUs); a grid that would
+        // not be resident takes the launch-by-launch path below.
         const int64_t nseg = (n + 1023) / 1024;
+        const int cus = usable_cus(s);
         const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(nseg, std::max(1, cus / 2)));
         const int segs = (int)((nseg + grid - 1) / grid);
-        if (segs <= 8 && nrows < (int64_t(1) << 31)) {
-            static bool attr_set = false;  // 64 KB static (the exact path's staging) + the window means
-            if (!attr_set) {
+        if (cus > 0 && segs <= 8 && nrows < (int64_t(1) << 31)) {
+            int dev = 0;
+            PU_TRY_HIP(hipGetDevice(&dev));
+            static std::atomic<uint64_t> attr_set{0};  // per device: 64 KB static (the exact
+                                                      // path's staging) + the window means
+            if (dev < 64 && !(attr_set.load() >> dev & 1)) {
                 PU_TRY_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(outlier_fused_kernel),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 8 * 1024 * (int)sizeof(double)));
-                attr_set = true;
+                attr_set.fetch_or(uint64_t(1) << dev);
             }
+            // resident workgroups per CU at this LDS size (cached per device and size)
+            static std::atomic<int> occ[64][9];
+            int per_cu = dev < 64 ? occ[dev][segs].load() : 0;
+            if (per_cu <= 0) {
+                PU_TRY_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                    &per_cu, reinterpret_cast<const void *>(outlier_fused_kernel), 256, (size_t)segs * 1024 * sizeof(double)));
+                if (dev < 64) occ[dev][segs].store(per_cu);
+            }
+            resident = (int64_t)per_cu * cus >= grid;
+        }
+        if (resident) {
             PU_TRY_HIP(hipMemsetAsync(st, 0, 128, s));
             OutlierBar *ob = reinterpret_cast<OutlierBar *>(reinterpret_cast<char *>(ws) + 64);
             hipLaunchKernelGGL(outlier_fused_kernel, dim3(grid), dim3(256), (size_t)segs * 1024 * sizeof(double), s, lc,

@@ -1012,6 +1012,7 @@ struct pu_plan {
     // stages {group begin, group end, item begin, item end}, build items, window records
     int group = 1, ngroups = 0, nslots_total = 0, raw_stride = 0, shape = SUB_WIDE;
     int dma8 = 0;  // subband plan stages 8-bit rows by LDS-DMA (rows must be 4-byte aligned)
+    int slot16 = 0;  // subband plan with 16-bit integer slots (8-bit rows)
     int base_bits = 31;  // subband DMA row words: base bits (24: per-channel cover above them)
     size_t slot_bytes = 0, zero_len = 0;
     int64_t exec_adds = 0, lds_traffic = 0;  // per launch (measurement: bench.py roofline)
@@ -2245,6 +2246,14 @@ size_t pu_plan_workspace_bytes(const pu_plan *p)
     return part_bytes(p) + sizeof(CertState) + (size_t)p->ndm * sizeof(int32_t);
 }
 
+// which kernel a plan's searches launch: 0 dedisp_kernel (channel order), 1 dedisp_f64_kernel,
+// 2 dedisp_sub_kernel (float32 slots), 3 dedisp_sub_kernel with 16-bit integer slots
+static int64_t plan_kernel(const pu_plan *p)
+{
+    if (p->group > 1) return p->slot16 ? 3 : 2;
+    return kVariants[p->variant].fsm ? 1 : 0;
+}
+
 int pu_plan_info(const pu_plan *p, int64_t *info, int n)
 {
     if (!p || !info) return 0;
@@ -2253,7 +2262,7 @@ int pu_plan_info(const pu_plan *p, int64_t *info, int n)
                          p->row_stride, (int64_t)p->lds_bytes, kVariants[p->variant].acc_f64, p->max_spread,
                          p->group, p->nslots_total, p->nstages, (int64_t)p->slot_bytes, p->raw_stride,
                          p->exec_adds, p->lds_traffic, p->cert_rechecked, p->cert_nan, p->cert_why[0],
-                         p->cert_why[1], p->cert_why[2], p->cert_us};
+                         p->cert_why[1], p->cert_why[2], p->cert_us, plan_kernel(p)};
     const int m = std::min<int>(n, (int)(sizeof v / sizeof v[0]));
     for (int k = 0; k < m; ++k) info[k] = v[k];
     return m;

@@ -77,7 +77,8 @@ SIGNATURES = {
 INFO_FIELDS = ("ndm", "dm_tiles", "time_tiles", "trials_per_tile", "time_tile", "chans_per_step",
                "row_stride", "lds_bytes", "acc_is_f64", "max_spread", "group", "slots", "stages",
                "slot_bytes", "raw_stride", "exec_adds", "lds_traffic", "cert_rechecked", "cert_nan", "cert_std", "cert_sign",
-               "cert_tie", "cert_us")
+               "cert_tie", "cert_us", "kernel")
+KERNEL_NAMES = ("dedisp_kernel", "dedisp_f64_kernel", "dedisp_sub_kernel", "dedisp_sub_kernel (u16 slots)")
 
 
 class HipBackendError(RuntimeError):

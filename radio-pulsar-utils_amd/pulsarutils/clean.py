@@ -287,6 +287,17 @@ def _certified_variability(means, moments, n, acc_f32, badchans_mask):
     return below | above | bad
 
 
+def _check_mask(badchans_mask, nrows):
+    """The channel mask as a boolean vector of ``nrows``; any other shape raises numpy's own
+    IndexError, as the reference's ``array[~badchans_mask]`` does (clean.py:77, :120) - the
+    kernels read exactly ``nrows`` mask bytes, so a short mask must never reach them."""
+    m = np.asarray(badchans_mask, dtype=bool)
+    if m.shape != (nrows,):
+        raise IndexError("boolean index did not match indexed array along axis 0; size of axis is %d but "
+                         "size of corresponding boolean axis is %s" % (nrows, m.shape[0] if m.ndim else m.shape))
+    return m
+
+
 def measure_channel_variability(array, badchans_mask=None):
     """clean.py:114-133: per-channel std outside [q2 - 2(q2-q1), q2 + 2(q3-q2)].
 
@@ -298,10 +309,10 @@ def measure_channel_variability(array, badchans_mask=None):
     std computed exactly (a second pass).  More than 4096 channels: the same
     certification on the host (_certified_variability).
     """
-    x = _hip.to_device(array)
     if badchans_mask is None:
-        badchans_mask = np.zeros(x.shape[0], dtype=bool)
-    badchans_mask = np.asarray(badchans_mask, dtype=bool)
+        badchans_mask = np.zeros(array.shape[0], dtype=bool)
+    badchans_mask = _check_mask(badchans_mask, array.shape[0])
+    x = _hip.to_device(array)
     t = _hip.torch()
     nrows = x.shape[0]
     v = _VAR[0]
@@ -417,7 +428,7 @@ def renormalize_device(x, badchans_mask=None, baseline_window=101, cut_outliers=
     s = _hip.stream_ptr()
     if badchans_mask is None:
         badchans_mask = np.zeros(nchan, dtype=bool)
-    bad_np = np.ascontiguousarray(np.asarray(badchans_mask, dtype=bool)).astype(np.uint8)
+    bad_np = np.ascontiguousarray(_check_mask(badchans_mask, nchan)).astype(np.uint8)
     bad = _device_mask(bad_np, dev)
     sigma = min(baseline_window, n // 100 * 2 + 1)
     dw, radius = _gaussian_weights_device(sigma, dev)

@@ -11,7 +11,8 @@ The reference's only parallelism is numba ``prange`` over independent DM trials
    (``collective``): ``"broadcast"`` (one RCCL broadcast from ``src``) or
    ``"scatter_allgather"`` (``src`` scatters 1/world of the chunk to every rank, then all
    ranks all-gather it: the second step's traffic runs over every xGMI link of the mesh
-   instead of leaving ``src``'s links alone; SURVEY §8e, DESIGN §5);
+   instead of leaving ``src``'s links alone).  The default
+   everywhere (``DEFAULT_COLLECTIVE``) is ``"scatter_allgather"``;
 2. each rank searches its contiguous slice of the trial grid on its own GPU,
 3. the per-trial statistics (max, std, snr, rebin) are all-gathered, so every rank
    ends with the reference's full-length result arrays.
@@ -35,7 +36,10 @@ def _hip_compute(data, dms, nchan, start_freq, bandwidth, sample_time, acc):
     return mx, sd, snr, win.to(mx.dtype)
 
 
-def broadcast_filterbank(data, src=0, group=None, collective="broadcast"):
+DEFAULT_COLLECTIVE = "scatter_allgather"
+
+
+def broadcast_filterbank(data, src=0, group=None, collective=DEFAULT_COLLECTIVE):
     """Give every rank ``src``'s (nchan, N) filterbank tensor, in place (contiguous data:
     the whole tensor is one :func:`exchange_chunk`; a padded tail goes through a staging
     copy when ``scatter_allgather`` needs a multiple of world elements)."""
@@ -73,7 +77,7 @@ def column_chunks(nsamples, chunks, quantum=1024):
 COLLECTIVES = ("broadcast", "scatter_allgather")
 
 
-def exchange_chunk(buf, piece, rank, src, world, group=None, collective="broadcast"):
+def exchange_chunk(buf, piece, rank, src, world, group=None, collective=DEFAULT_COLLECTIVE):
     """Make every rank's ``buf`` (1-D, contiguous) equal ``src``'s.
 
     ``"broadcast"``: one broadcast from ``src``.  ``"scatter_allgather"``: ``buf``'s length
@@ -131,6 +135,40 @@ class PlanSearcher:
             o.record_stream(stream)
 
 
+class PhaseEvents:
+    """HIP events around the phases of one pipelined step (``pipelined_broadcast_search``'s
+    ``phases``): ``exchange`` and ``unpack`` per chunk on the communication stream,
+    ``search`` per chunk (the tile-range launches) on the compute stream, ``finalize``.
+    :meth:`times_ms` (after a synchronize) gives each phase's per-chunk durations and, as
+    ``exposed_tail_ms``, the time from the last chunk's unpack end to the finalize end -
+    the part of the search the exchange could not hide."""
+
+    def __init__(self):
+        self.ev = {}
+
+    def mark(self, name, stream, end=False):
+        import torch
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(stream)
+        self.ev.setdefault(name, []).append((e, end))
+
+    def _spans(self, name):
+        evs = self.ev.get(name, [])
+        return [(evs[i][0], evs[i + 1][0]) for i in range(0, len(evs) - 1, 2)]
+
+    def times_ms(self):
+        out = {name: [round(a.elapsed_time(b), 4) for a, b in self._spans(name)] for name in self.ev}
+        res = {f"{k}_ms": v for k, v in out.items()}
+        for k, v in out.items():
+            res[f"{k}_total_ms"] = round(float(sum(v)), 4)
+        ex, fin = self._spans("exchange"), self._spans("finalize")
+        last = self._spans("unpack")[-1][1] if self._spans("unpack") else (ex[-1][1] if ex else None)
+        if ex and fin:
+            res["step_span_ms"] = round(ex[0][0].elapsed_time(fin[-1][1]), 4)
+            res["exposed_tail_ms"] = round(last.elapsed_time(fin[-1][1]), 4)
+        return res
+
+
 _MASKED = {}  # (device index, reserved CUs) -> MaskedStream, kept for the process
 
 
@@ -147,7 +185,7 @@ def _masked_stream(reserve, dev):
 
 
 def pipelined_broadcast_search(data, plan, out=None, workspace=None, src=0, chunks=8, group=None, searcher=None,
-                               reserve_cus=0, collective="broadcast"):
+                               reserve_cus=0, collective=DEFAULT_COLLECTIVE, phases=None):
     """Distribute ``data`` from ``src`` in time chunks while searching it with ``plan``.
 
     Chunk k (a range of whole time tiles, all channels) is packed into a contiguous
@@ -167,6 +205,16 @@ def pipelined_broadcast_search(data, plan, out=None, workspace=None, src=0, chun
     (scripts/overlap_probe.py, profiles/r03/overlap_probe_r3b.json) shows copy kernels on
     a second stream getting 2.2 TB/s beside the unmasked search, and an 8-CU mask slowing
     the search alone by 15 % (15.6 -> 18.0 ms) without speeding the copies.
+
+    ``phases`` (device data only): a :class:`PhaseEvents` that records HIP events around each
+    chunk's exchange and unpack (communication stream), each chunk's tile searches (compute
+    stream) and the finalize; :meth:`PhaseEvents.times_ms` reads them after a synchronize.
+
+    Receiving ranks copy each landed chunk from the contiguous staging buffer into the
+    strided column range ``data[:, c0:c1]`` (the ``unpack`` phase): RCCL moves contiguous
+    buffers only, and the kernels read rows of ``data`` at its row stride, so a column chunk
+    cannot land in place.  The copy runs on the communication stream, overlapped with the
+    search of the chunks already landed; ``phases`` measures it.
 
     ``searcher`` replaces the HIP work (an object with ``ntiles``, ``ready(landed)``,
     ``tiles(data, begin, end, stream)`` and ``finalize(data, stream)``): with a CPU
@@ -218,12 +266,19 @@ def pipelined_broadcast_search(data, plan, out=None, workspace=None, src=0, chun
                 blen = -(-nchan * (c1 - c0) // world) * world
                 flat = staging[:blen]
                 buf = flat[:nchan * (c1 - c0)].view(nchan, c1 - c0)  # contiguous
+                if phases is not None:
+                    phases.mark("exchange", comm)
                 if rank == src:
                     buf.copy_(data[:, c0:c1])
                 exchange_chunk(flat, piece[:blen // world] if piece is not None else None, rank, src, world,
                                group=group, collective=collective)
+                if phases is not None:
+                    phases.mark("exchange", comm, end=True)
+                    phases.mark("unpack", comm)
                 if rank != src:
                     data[:, c0:c1].copy_(buf)
+                if phases is not None:
+                    phases.mark("unpack", comm, end=True)
             ev = None
             if cuda:
                 ev = torch.cuda.Event()
@@ -235,8 +290,12 @@ def pipelined_broadcast_search(data, plan, out=None, workspace=None, src=0, chun
         ready = searcher.ready(c1) & ~done
         idx = np.flatnonzero(ready)
         # contiguous runs of ready tiles, one launch each
+        if phases is not None:
+            phases.mark("search", tstream)
         for run in np.split(idx, np.flatnonzero(np.diff(idx) != 1) + 1) if idx.size else []:
             searcher.tiles(data, int(run[0]), int(run[-1]) + 1, stream=tstream)
+        if phases is not None:
+            phases.mark("search", tstream, end=True)
         done |= ready
         if masked is not None and k + 2 == len(bounds):
             comp.wait_stream(masked.stream)  # the unmasked stream takes over for the last chunk
@@ -250,7 +309,11 @@ def pipelined_broadcast_search(data, plan, out=None, workspace=None, src=0, chun
         return None
     if not done.all():
         raise RuntimeError("pipelined search: time tiles left unsearched")
+    if phases is not None:
+        phases.mark("finalize", comp)
     res = searcher.finalize(data, stream=comp)
+    if phases is not None:
+        phases.mark("finalize", comp, end=True)
     if cuda:
         if hasattr(searcher, "streams_done"):
             searcher.streams_done(comp)
@@ -261,7 +324,7 @@ def pipelined_broadcast_search(data, plan, out=None, workspace=None, src=0, chun
 
 
 def sharded_search(data, trial_DMs, nchan, start_freq, bandwidth, sample_time, group=None, acc=None,
-                   compute=None, broadcast=True, src=0, pipelined=False, chunks=8, collective="broadcast"):
+                   compute=None, broadcast=True, src=0, pipelined=False, chunks=8, collective=DEFAULT_COLLECTIVE):
     """Distributed ``_dedispersion_search``: returns (max, std, snr, rebin[int32]) numpy arrays
     covering ALL trials, on every rank.
 

@@ -5,7 +5,8 @@
 # (FETCH_SIZE, WRITE_SIZE: one rocprofv3 --pmc run each) next to a bench line of the same
 # command, summarised by scripts/pmc_json.py.  Each GPU step has its own time limit; the
 # script stops at the first step that fails.
-#   NOTEST=1: skip the test suite.  PMC="C2 C5 C3 C3_625": the PMC configs.  CFGS=1: also
+#   NOTEST=1: skip the test suite.  NOSMOKE=1: skip __graft_entry__.smoke().  SQ=1: SQ counter
+#   passes of the C3 625 shard.  MR=1: a 2-rank rehearsal of the N > 1 bench on this GPU.  PMC="C2 C5 C3 C3_625": the PMC configs.  CFGS=1: also
 #   bench lines for C1/C5/C3 (5000) / the C3 625-trial shard.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -16,9 +17,13 @@ mkdir -p $OUT
 if [ -z "$NOTEST" ]; then
   timeout -k 10 1000 python -u -m pytest tests -v -m gpu -x --timeout 400 --timeout-method thread -p no:cacheprovider > $OUT/gpu_tests.log 2>&1 || exit $?
 fi
+if [ -z "$NOSMOKE" ]; then
+  timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit $?
+fi
 if [ -z "$NOBENCH" ]; then
   timeout -k 10 500 python -u bench.py --steps 20 --warmup 2 > $OUT/bench.json 2> $OUT/bench.err || exit $?
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-c3-strong > $OUT/prof.log 2>&1 || exit $?
+  python3 scripts/warm_stats.py $OUT/prof --skip 1 > $OUT/rocprof_warm_stats.csv || exit $?
 fi
 args_of() {
   case $1 in
@@ -38,6 +43,23 @@ for cfg in ${PMC:-}; do
   timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $D/p2 -o run -- python3 bench.py $A --steps 1 --warmup 1 --no-cpu-baseline --no-clean --no-c3-strong > $D/p2.log 2>&1 || exit $?
   python3 scripts/pmc_json.py $D $cfg $D/bench.json > $D/pmc_json.log 2>&1 || exit $?
 done
+if [ -n "$SQ" ]; then
+  # SQ counter passes of the C3 625-trial shard (scalar vs vector issue) at this source
+  A=$(args_of C3_625)
+  i=0
+  for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY" \
+             "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"; do
+    i=$((i+1))
+    timeout -s KILL 300 rocprofv3 --pmc $set --output-format csv -d $OUT/sq_c3_625/p$i -o run -- python3 bench.py $A --steps 1 --warmup 1 --no-cpu-baseline --no-clean --no-c3-strong --no-acc-f64 > $OUT/sq_c3_625_p$i.log 2>&1 || exit $?
+  done
+fi
+if [ -n "$MR" ]; then
+  # the N > 1 bench path rehearsed with 2 ranks on this one GPU (gloo: both ranks share the
+  # device), small config
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29533 bench.py --gpus 2 --config C5 --dist-backend gloo --steps 2 --warmup 1 --bcast-chunks 4 \
+    > $OUT/mr_bench_c5.json 2> $OUT/mr_bench_c5.err || exit $?
+fi
 if [ -n "$CFGS" ]; then
   for cfg in C1 C5 C3 C3_625; do
     A=$(args_of $cfg)

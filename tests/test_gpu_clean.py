@@ -435,6 +435,27 @@ def test_noisy_channels_nonfinite_flag(gpu, bad):
     np.testing.assert_array_equal(C.get_noisier_channels(x), _noisy_host(x.mean(1)))
 
 
+@pytest.mark.parametrize("nchan", [16, 600, 1500])
+def test_noisy_channels_overflowing_differences(gpu, nchan):
+    """a finite float32 spectrum whose np.diff overflows to +-inf (means of
+    +-3e38) makes the median of the differences NaN (inf - inf), which the device's register
+    sorts (v_min_f64 / v_max_f64 drop NaN) cannot order: both kernels raise the flag and the
+    masks come from the host's numpy / scipy arithmetic - the same as the reference's."""
+    from pulsarutils import _hip
+    spec = np.where(np.arange(nchan) % 2 == 0, 3e38, -3e38).astype(np.float32)
+    assert np.isfinite(spec).all() and not np.isfinite(np.diff(spec)).all()
+    mask, flag = _noisy_device(spec)
+    assert flag == 1
+    x = np.repeat(spec[:, None], 1, axis=1)
+    np.testing.assert_array_equal(C.get_noisier_channels(x), _noisy_host(spec))
+    if nchan <= 1024:
+        xd = _hip.to_device(x)
+        C.invalidate_channel_means()
+        np.testing.assert_array_equal(C.get_noisier_channels(xd), _noisy_host(spec))
+        np.testing.assert_array_equal(C.measure_channel_variability(xd),
+                                      co.channel_variability(x, badchans_mask=None))
+
+
 def test_noisy_channels_wide_band_host_path(gpu):
     """More channels than one workgroup decides (4097): the host path, same mask."""
     x = np.random.default_rng(3).normal(0, 1, (4097, 256)).astype(np.float32)

@@ -308,8 +308,10 @@ def test_search_ragged_small(gpu, dt, group):
 
 
 @pytest.mark.parametrize("name", ["C2", "C5"])
-def test_search_full_size_sampled_trials(gpu, golden, name):
-    """Full-size configs on device data; a spread of trials re-done by the C oracle."""
+def test_search_full_size_all_trials(gpu, golden, name):
+    """Full-size configs on device data; EVERY trial of the grid re-done by the C oracle
+    (C2: 1000 trials x 2^20 samples, ~25 s on 16 threads; C5: 500 trials, < 1 s) - the
+    whole table against SURVEY §8a's bars, argmax over the whole grid."""
     import torch
     from pulsarutils import synth
     arrays, _ = golden
@@ -318,26 +320,36 @@ def test_search_full_size_sampled_trials(gpu, golden, name):
     dms = arrays[f"plan_{name}"]
     (mx, sd, snr, win), plan = D.search_device(xd, dms, c.nchan, c.start_freq, c.bandwidth, c.tsamp)
     torch.cuda.synchronize()
-    snr = snr.cpu().numpy()
+    snr, mx, sd, win = (v.cpu().numpy() for v in (snr, mx, sd, win))
     best = dms[np.argmax(snr)]
     assert abs(best - c.pulse_dm) < 0.5, (best, c.pulse_dm)
     x = xd.cpu().numpy()
-    idx = sampled_trials(snr, 32)
-    omx, osd, osnr, owin = oracle.search(x, dms[idx], c.start_freq, c.bandwidth, c.tsamp, nthreads=16)
-    np.testing.assert_allclose(snr[idx], osnr, rtol=1e-5)
+    del xd
+    torch.cuda.empty_cache()
+    omx, osd, osnr, owin, osw = oracle.search(x, dms, c.start_freq, c.bandwidth, c.tsamp, nthreads=16,
+                                              return_width_snr=True)
+    np.testing.assert_allclose(snr, osnr, rtol=1e-5)
     # max and std from the per-sample float32 bound E_t = nchan 2^-24 sum_c |x_c[t + s_c]|
     # (module docstring): the max of the series moves by <= max_t E_t, the mean by <= its
     # mean, so max - mean by <= 2 max_t E_t; std is 1-Lipschitz in the sup norm (<= max_t
-    # E_t).  Plus the statistics' own float64/float32 rounding, 1e-6 relative.
-    _, _, _, _, ad = oracle.search(np.abs(x), dms[idx], c.start_freq, c.bandwidth, c.tsamp, nthreads=16,
-                                   return_dedisp=True)
-    emax = c.nchan * 2.0 ** -24 * ad.max(axis=1)
-    del ad
-    assert np.all(np.abs(mx.cpu().numpy()[idx] - omx) <= 2 * emax + 1e-6 * np.abs(omx))
-    assert np.all(np.abs(sd.cpu().numpy()[idx] - osd) <= emax + 1e-6 * osd)
-    np.testing.assert_array_equal(win.cpu().numpy()[idx], owin)
-    # argmax DM over the sample agrees (the top 5 by S/N are in it)
-    assert idx[np.argmax(snr[idx])] == idx[np.argmax(osnr)]
+    # E_t).  Plus the statistics' own float64/float32 rounding, 1e-6 relative.  The inputs
+    # are non-negative (|N(0, 0.5)| + pulse), so sum_c |x_c[t + s_c]| is the series itself
+    # and its maximum is the oracle's max(d) + mean (mean = sum_c mean_c for every trial).
+    assert float(x.min()) >= 0.0
+    mu = float(x.sum(dtype=np.float64)) / x.shape[1]
+    emax = c.nchan * 2.0 ** -24 * (omx + mu) * (1 + 1e-6)
+    assert np.all(np.abs(mx - omx) <= 2 * emax + 1e-6 * np.abs(omx))
+    assert np.all(np.abs(sd - osd) <= emax + 1e-6 * osd)
+    # rebin equal for every trial whose best and second-best window S/N are more than 1e-5
+    # apart (the oracle's per-width S/N of each trial decides which trials are ties)
+    srt = np.sort(osw, axis=1)
+    tie = (srt[:, -1] - srt[:, -2]) <= 1e-5 * np.abs(srt[:, -1])
+    assert np.array_equal(win[~tie], owin[~tie]), np.nonzero((win != owin) & ~tie)[0][:10]
+    assert tie.sum() <= max(2, dms.size // 100), int(tie.sum())
+    # argmax over the whole grid (unless the top two S/N are within the tolerance)
+    top2 = np.sort(osnr)[-2:]
+    if top2[1] - top2[0] > 1e-5 * top2[1]:
+        assert np.argmax(snr) == np.argmax(osnr)
 
 
 def sampled_trials(snr, n):

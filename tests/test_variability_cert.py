@@ -122,3 +122,18 @@ def test_moment_error_bound_covers_serial_tail(k):
     Vx = S2 - 2 * Fraction(dm) * S1 + n * Fraction(dm) ** 2
     eV = (s2 + 2.0 * abs(dm) * np.sqrt(n * s2) + n * dm * dm) * moment_error_factor(n)
     assert abs(Fraction(V) - Vx) <= Fraction(eV)
+
+
+@pytest.mark.parametrize("length", [7, 9, 0])
+def test_channel_mask_length_raises_like_numpy(length):
+    """A channel mask whose length is not nchan raises numpy's IndexError before anything
+    reaches the device (the kernels read exactly nchan mask bytes), as the reference's
+    ``spec[~badchans_mask]`` does (clean.py:120)."""
+    from pulsarutils import clean
+    x = np.ones((8, 64), np.float32)
+    if length:  # (numpy lets an empty boolean index through; the reference then fails at
+        #          ordered[spec.size // 4] - here the length check raises first)
+        with pytest.raises(IndexError):
+            np.std(x, axis=1)[~np.zeros(length, bool)]
+    with pytest.raises(IndexError, match="boolean index did not match"):
+        clean.measure_channel_variability(x, badchans_mask=np.zeros(length, bool))
