@@ -381,6 +381,162 @@ __device__ __forceinline__ void group_trials(f32x2 (&acc)[C::D][C::J], const Rec
     }
 }
 
+// ---- 16-bit integer slots (8-bit input, time tile 256: DESIGN.md §4.1b).  A slot of an
+// 8-bit group is a sum of <= G bytes, an integer <= G x 255, kept as u16 in four alignment
+// copies (copy s holds R[i + s] at element i), so every window - 256 samples, four per
+// lane - is ONE ds_read_b64 at an 8-byte-aligned address: half the sum's LDS reads of the
+// float32 slots (two ds_read_b64 per window).  Lane l owns samples 4 l .. 4 l + 3 of its D
+// trials in packed u16 accumulators `lo` (added by v_pk_add_u16: every add exact while
+// the total since the last flush stays < 2^16) and `hi` (units of 256): every <= F groups
+// (F G 255 + 255 < 2^16) `hi += lo >> 8, lo &= 255` - then hi 256 + lo is the exact
+// integer sum (< nchan 255 < 2^24), converted to float32 once per item.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+#define PU_WAIT1_CASE(N) asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(w) : : "memory");
+template <int N>
+__device__ __forceinline__ void wait_window1(double &w)
+{
+    static_assert(N >= 0 && N <= 7, "lgkmcnt");
+    if constexpr (N == 7) { PU_WAIT1_CASE(7) }
+    else if constexpr (N == 6) { PU_WAIT1_CASE(6) }
+    else if constexpr (N == 5) { PU_WAIT1_CASE(5) }
+    else if constexpr (N == 4) { PU_WAIT1_CASE(4) }
+    else if constexpr (N == 3) { PU_WAIT1_CASE(3) }
+    else if constexpr (N == 2) { PU_WAIT1_CASE(2) }
+    else if constexpr (N == 1) { PU_WAIT1_CASE(1) }
+    else { PU_WAIT1_CASE(0) }
+}
+#undef PU_WAIT1_CASE
+
+// s_waitcnt lgkmcnt(N) that "defines" v (the value it guards), N in [0, 15]
+#define PU_WAITV_CASE(N) else if constexpr (N0 == N) asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(v) : : "memory");
+template <int N0>
+__device__ __forceinline__ void wait_lgkm(uint32_t &v)
+{
+    static_assert(N0 >= 0 && N0 <= 15, "lgkmcnt");
+    if constexpr (N0 == 0) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v) : : "memory");
+    PU_WAITV_CASE(1) PU_WAITV_CASE(2) PU_WAITV_CASE(3) PU_WAITV_CASE(4) PU_WAITV_CASE(5) PU_WAITV_CASE(6)
+    PU_WAITV_CASE(7) PU_WAITV_CASE(8) PU_WAITV_CASE(9) PU_WAITV_CASE(10) PU_WAITV_CASE(11) PU_WAITV_CASE(12)
+    PU_WAITV_CASE(13) PU_WAITV_CASE(14) PU_WAITV_CASE(15)
+}
+#undef PU_WAITV_CASE
+
+// 16-bit slot build, one chunk of 128 elements: lane l's two elements 128 c + 2 l (+ 1) as
+// the byte sums of the G channels (addresses ad[q], reads rb in flight).
+template <int G, int C>
+__device__ __forceinline__ void s16_issue(uint32_t (&rb)[G][2], const uint32_t (&ad)[G])
+{
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(rb[q][0]) : "v"(ad[q]), "i"(128 * C) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(rb[q][1]) : "v"(ad[q]), "i"(128 * C + 1) : "memory");
+    }
+}
+
+// Read i of chunk C (channel i / 2, byte i % 2): wait until it landed - the reads complete
+// in issue order, so it is the oldest outstanding when the 2 G - 1 later reads of this chunk
+// and (NEXT) the i already re-issued for chunk C + 1 may still be in flight: lgkmcnt(2 G -
+// 1), or 2 G - 1 - i for the last chunk (an outstanding scalar load only lengthens the
+// wait) - add it, and (NEXT) re-issue its register for chunk C + 1.
+template <int G, int C, bool NEXT, int I>
+__device__ __forceinline__ void s16_step(uint32_t (&rb)[G][2], const uint32_t (&ad)[G], uint32_t &s0, uint32_t &s1)
+{
+    if constexpr (I < 2 * G) {
+        constexpr int q = I >> 1, e = I & 1;
+        static_assert(2 * G - 1 <= 15, "lgkmcnt");
+        wait_lgkm<NEXT ? 2 * G - 1 : 2 * G - 1 - I>(rb[q][e]);
+        if constexpr (e == 0)
+            s0 += rb[q][e];
+        else
+            s1 += rb[q][e];
+        if constexpr (NEXT)
+            asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(rb[q][e]) : "v"(ad[q]), "i"(128 * (C + 1) + e) : "memory");
+        s16_step<G, C, NEXT, I + 1>(rb, ad, s0, s1);
+    }
+}
+
+template <int G, int C, bool NEXT>
+__device__ __forceinline__ uint32_t s16_chunk(uint32_t (&rb)[G][2], const uint32_t (&ad)[G])
+{
+    uint32_t s0 = 0, s1 = 0;
+    s16_step<G, C, NEXT, 0>(rb, ad, s0, s1);
+    return s0 | (s1 << 16);
+}
+
+__device__ __forceinline__ void issue_window1(double &w, uint32_t addr)
+{
+    asm volatile("ds_read_b64 %0, %1" : "=&v"(w) : "v"(addr) : "memory");
+}
+
+// One group's contribution to the wave's D trials from 16-bit slots: one window read per
+// trial, issued A trials ahead of its two v_pk_add_u16.
+template <int D, int A, int I, typename RecT>
+__device__ __forceinline__ void trials16_step(u16x2 (&lo)[D][2], double (&w)[A + 1], const RecT &rec, uint32_t base)
+{
+    if constexpr (I < D) {
+        if constexpr (I + A < D) issue_window1(w[(I + A) % (A + 1)], base + rec[I + A]);
+        constexpr int ahead = D - 1 - I < A ? D - 1 - I : A;
+        double &wd = w[I % (A + 1)];
+        wait_window1<ahead>(wd);
+        const u32x2 v = __builtin_bit_cast(u32x2, wd);
+        lo[I][0] += __builtin_bit_cast(u16x2, v.x);
+        lo[I][1] += __builtin_bit_cast(u16x2, v.y);
+        asm volatile("" : "+v"(lo[I][0]), "+v"(lo[I][1]));
+        trials16_step<D, A, I + 1>(lo, w, rec, base);
+    }
+}
+
+template <class C, typename RecT>
+__device__ __forceinline__ void group_trials16(u16x2 (&lo)[C::D][2], const RecT rec, uint32_t base)
+{
+    constexpr int D = C::D, A = 5;
+    double w[A + 1];
+#pragma unroll
+    for (int d = 0; d < A && d < D; ++d) issue_window1(w[d], base + rec[d]);
+    trials16_step<D, A, 0>(lo, w, rec, base);
+}
+
+// hi += lo >> 8, lo &= 255 (exact: lo < 2^16; hi counts 256s, < nchan < 2^16)
+template <int D>
+__device__ __forceinline__ void flush16(u16x2 (&lo)[D][2], u16x2 (&hi)[D][2])
+{
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            hi[d][k] += lo[d][k] >> (u16x2){8, 8};
+            lo[d][k] &= (u16x2){0xff, 0xff};
+        }
+}
+
+// The exact sums as float32 in the float slots' lane layout (lane l: samples 128 j + 2 l +
+// e), which the epilogues and write_outputs take: sample 128 j + 2 l + e lives in lane
+// 32 j + l / 2, element 2 (l & 1) + e - four ds_bpermute per (trial, j) and a select.
+template <int D>
+__device__ __forceinline__ void s16_to_pairs(const u16x2 (&lo)[D][2], const u16x2 (&hi)[D][2], f32x2 (&acc)[D][2],
+                                             int lane)
+{
+    const bool odd = lane & 1;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        float v[4];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            v[2 * k] = (float)((uint32_t)hi[d][k].x * 256u + (uint32_t)lo[d][k].x);
+            v[2 * k + 1] = (float)((uint32_t)hi[d][k].y * 256u + (uint32_t)lo[d][k].y);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int src = 4 * (32 * j + (lane >> 1));
+            float g[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                g[e] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src, __builtin_bit_cast(int, v[e])));
+            acc[d][j] = odd ? f32x2{g[2], g[3]} : f32x2{g[0], g[1]};
+        }
+    }
+}
+
 // LDS-DMA of one 8-bit channel-row window [start, start + cover) mod n into dst, start
 // and n multiples of 4 (the planner folds each row's misalignment into the slot
 // sources): 1 KiB pieces while contiguous, per-lane modular dwords if it wraps.
@@ -415,7 +571,7 @@ __device__ __forceinline__ void dma_row_u8(unsigned char *dst, const unsigned ch
 // and float64 builds read global memory.
 // One (DM tile, time tile) work item of the subband kernel: logical index wg; first =
 // this workgroup's first item (it writes the zero row, which no item overwrites).
-template <class C, typename Tin, int G, bool PLANE, bool STATS, bool DMA8>
+template <class C, typename Tin, int G, bool PLANE, bool STATS, bool DMA8, bool S16>
 __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ tiles,
                                          const i32x2 *__restrict__ tile_stages, const i32x4 *__restrict__ stages,
                                          const int32_t *__restrict__ slots, const int32_t *__restrict__ base_tab,
@@ -456,11 +612,24 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
     const float *raw_lds = reinterpret_cast<const float *>(smem);
     const unsigned char *raw_lds8 = smem;
 
+    static_assert(!S16 || (kDma && EB == 1 && C::K == 4), "16-bit slots: 8-bit DMA rows, 256-sample tiles");
     f32x2 acc2[D][C::J];
+    if constexpr (!S16) {
 #pragma unroll
-    for (int d = 0; d < D; ++d)
+        for (int d = 0; d < D; ++d)
 #pragma unroll
-        for (int m = 0; m < C::J; ++m) acc2[d][m] = f32x2{0.0f, 0.0f};
+            for (int m = 0; m < C::J; ++m) acc2[d][m] = f32x2{0.0f, 0.0f};
+    }
+    // 16-bit slots: packed u16 accumulators, flushed every <= F16 groups (see flush16)
+    constexpr int F16 = (65535 - 255) / (G * 255);
+    u16x2 lo16[S16 ? D : 1][2], hi16[S16 ? D : 1][2];
+    if constexpr (S16) {
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+#pragma unroll
+            for (int k = 0; k < 2; ++k) lo16[d][k] = hi16[d][k] = u16x2{0, 0};
+    }
+    int gc16 = 0;  // groups added since the last flush
 
     const rec_t *recs = reinterpret_cast<const rec_t *>(rec_tab) + (size_t)dt * a.ngroups * W + wave;
     if constexpr (kDma) {
@@ -635,6 +804,55 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
         }
     };
 
+    // ---- 16-bit slots (S16): one slot in chunks of 128 elements, lane l building elements
+    // 128 u + 2 l and + 1 of chunk u (two byte reads per channel, summed as integers) packed
+    // as one u16 pair E_u; the odd-shifted pair (R[2k + 1], R[2k + 2]) is E_u's high half
+    // with the next lane's low half (DPP wave_shl:1; lane 63 takes chunk u + 1's lane 0 by
+    // wave_rol:1).  Stores by ds_write_addtid_b32: E_u to copy 0 and, 4 bytes down, copy 2;
+    // O_u to copy 1 and, 4 bytes down, copy 3 (element i of copy s is R[i + s]).  Chunks
+    // 0-2 always (the planner's copies hold >= 384 elements, len <= 512), chunk 3 when len >
+    // 384; reads of chunk c + 1 in flight while chunk c is summed.
+    auto slot16 = [&](const meta_t &m) {
+        const bool four = m[0] > 384;
+        auto odd = [&](uint32_t e, uint32_t enext) {  // (R[2k + 1], R[2k + 2]) of lane k
+            const uint32_t x = (uint32_t)__builtin_amdgcn_mov_dpp((int)enext, 0x134, 0xf, 0xf, false);  // wave_rol:1
+            const uint32_t y = (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)e, 0x130, 0xf, 0xf, false);  // wave_shl:1
+            return __builtin_amdgcn_alignbit(y, e, 16);
+        };
+        // per channel the lane's byte address; 2 G byte reads per chunk (ds_read_u8 in inline
+        // asm: the order kept by s16_chunk holds ~15 in flight in 16 registers - each value is
+        // added, then its register takes the next chunk's read of the same channel and byte)
+        uint32_t ad[G];
+#pragma unroll
+        for (int q = 0; q < G; ++q) ad[q] = smem_addr + (uint32_t)m[4 + q] + 2u * (uint32_t)lane;
+        uint32_t rb[G][2];
+        s16_issue<G, 0>(rb, ad);
+        const uint32_t e0 = s16_chunk<G, 0, true>(rb, ad);
+        const uint32_t e1 = s16_chunk<G, 1, true>(rb, ad);
+        uint32_t e2, e3 = 0;
+        if (four) {
+            e2 = s16_chunk<G, 2, true>(rb, ad);
+            e3 = s16_chunk<G, 3, false>(rb, ad);
+        } else {
+            e2 = s16_chunk<G, 2, false>(rb, ad);
+        }
+        uint32_t o0 = odd(e0, e1), o1 = odd(e1, e2), o2 = odd(e2, e3), o3 = four ? odd(e3, e3) : 0u;
+        asm volatile("" : "+v"(o0), "+v"(o1), "+v"(o2), "+v"(o3));
+        const uint32_t c0 = lds_base + (uint32_t)m[1];
+        const uint32_t cbu = (uint32_t)copy_bytes;
+        auto store = [&](uint32_t base, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
+            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(base) : "memory");
+            asm volatile("ds_write_addtid_b32 %0 offset:0" : : "v"(v0) : "memory");
+            asm volatile("ds_write_addtid_b32 %0 offset:256" : : "v"(v1) : "memory");
+            asm volatile("ds_write_addtid_b32 %0 offset:512" : : "v"(v2) : "memory");
+            if (four) asm volatile("ds_write_addtid_b32 %0 offset:768" : : "v"(v3) : "memory");
+        };
+        store(c0, e0, e1, e2, e3);
+        store(c0 + 2u * cbu - 4u, e0, e1, e2, e3);
+        store(c0 + cbu, o0, o1, o2, o3);
+        store(c0 + 3u * cbu - 4u, o0, o1, o2, o3);
+    };
+
     // ---- build the stage's slots, one per wave at a time: R[i] (i < len) at copy 0 [i]
     // and copy 1 [i - 1] (copy 1's element -1 lands in copy 0's padding).  (Splitting a
     // slot over waves to balance the ~20 slots of a stage over 16 waves was measured
@@ -661,10 +879,16 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
         const meta_t *mp = reinterpret_cast<const meta_t *>(slots) + (size_t)(st.z + wave + W);
         for (int s = st.z + wave; s < st.w; s += 2 * W, mp += 2 * W) {
             meta_t mb = ld_uniform(mp);
-            slot(ma);
+            if constexpr (S16)
+                slot16(ma);
+            else
+                slot(ma);
             if (s + W >= st.w) break;
             ma = ld_uniform(mp + W);
-            slot(mb);
+            if constexpr (S16)
+                slot16(mb);
+            else
+                slot(mb);
         }
     };
 
@@ -732,11 +956,23 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
             const int gl = st.y - 1;
             for (int g = st.x; g < st.y; g += 2) {
                 rec_t rb = ld_uniform(recs + (size_t)min(g + 1, gl) * W);
-                group_trials<C>(acc2, ra, sb);
+                if constexpr (S16) {
+                    if (gc16 + 2 > F16) {
+                        flush16<D>(lo16, hi16);
+                        gc16 = 0;
+                    }
+                    gc16 += 2;
+                    group_trials16<C>(lo16, ra, sb);
+                } else {
+                    group_trials<C>(acc2, ra, sb);
+                }
                 asm volatile("" : "+s"(rb));
                 if (g + 1 > gl) break;
                 ra = ld_uniform(recs + (size_t)min(g + 2, gl) * W);
-                group_trials<C>(acc2, rb, sb);
+                if constexpr (S16)
+                    group_trials16<C>(lo16, rb, sb);
+                else
+                    group_trials<C>(acc2, rb, sb);
                 asm volatile("" : "+s"(ra));
             }
         }
@@ -744,6 +980,9 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
         PU_PHASE(5);
         st = st1;
         st1 = st2;
+    }
+    if constexpr (S16) {
+        if (active) s16_to_pairs<D>(lo16, hi16, acc2, lane);
     }
     if constexpr (STATS && !PLANE) {
         if (active && !(skip & 8) && t0 + TT <= n) {
@@ -782,13 +1021,13 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
 // items b, b + grid, ... - measured slower at C2, 16.68 vs 16.19 ms: the hardware's
 // dynamic dispatch of the next workgroup to whichever CU frees first beats a static
 // round-robin; and its loop state cost the C3 instantiation scratch spills.)
-template <class C, typename Tin, int G, bool PLANE, bool STATS, bool DMA8>
+template <class C, typename Tin, int G, bool PLANE, bool STATS, bool DMA8, bool S16 = false>
 __global__ void __launch_bounds__(C::THREADS, 4)
 dedisp_sub_kernel(SubArgs a, const i32x4 *__restrict__ tiles, const i32x2 *__restrict__ tile_stages,
                   const i32x4 *__restrict__ stages, const int32_t *__restrict__ slots,
                   const int32_t *__restrict__ base_tab, const uint32_t *__restrict__ rec_tab)
 {
-    sub_item<C, Tin, G, PLANE, STATS, DMA8>(a, tiles, tile_stages, stages, slots, base_tab, rec_tab,
+    sub_item<C, Tin, G, PLANE, STATS, DMA8, S16>(a, tiles, tile_stages, stages, slots, base_tab, rec_tab,
                                             pu::xcd_remap(blockIdx.x, gridDim.x), true);
 }
 
@@ -1019,7 +1258,7 @@ struct pu_plan {
     std::vector<int32_t> tile_first, tile_count;  // DM tiles in launch order (pu_plan_dm_tiles)
     int64_t nstages = 0;
     int dt_major = 0;  // subband item order (SubArgs::dt_major)
-    int opt_u8_dma = -1, opt_dt_major = -1;  // pu_plan_opts (planner inputs)
+    int opt_u8_dma = -1, opt_dt_major = -1, opt_slot16 = 1;  // pu_plan_opts (planner inputs)
     i32x4 *d_tiles = nullptr, *d_stages = nullptr;
     i32x2 *d_tile_stages = nullptr;
     int32_t *d_slots = nullptr;
@@ -1121,6 +1360,11 @@ int launch_sub(const pu_plan *p, const DedispArgs &a, bool plane, hipStream_t s)
         return pu::launch_check("dedisp_sub_kernel");
     };
     if constexpr (std::is_same<Tin, uint8_t>::value) {
+        if constexpr (C::K == 4) {
+            if (p->slot16)
+                return plane ? go(dedisp_sub_kernel<C, Tin, G, true, false, true, true>)
+                             : go(dedisp_sub_kernel<C, Tin, G, false, true, true, true>);
+        }
         if (p->dma8)
             return plane ? go(dedisp_sub_kernel<C, Tin, G, true, false, true>)
                          : go(dedisp_sub_kernel<C, Tin, G, false, true, true>);
@@ -1462,6 +1706,7 @@ int plan_channels(pu_plan *p, const int64_t *shifts, size_t budget)
 // trial's group does not fit the LDS budget (the caller then tries a smaller G, then
 // channel mode).
 constexpr int64_t kSubMaxSpread = 2048;
+constexpr int64_t kS16Span = 254;  // 16-bit slots: TT + span + 2 <= 512 elements (four build chunks)
 constexpr int64_t kDtMajorItems = 16 * 256;  // below this many items per launch: DM-tile-major order
 
 struct SubSlot {
@@ -1484,6 +1729,10 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     dma8 = dma8 && pu::knob("PU_U8_DMA", p->opt_u8_dma) != 0;
     const bool dma = p->dtype == PU_F32 || dma8;
     const int64_t eb = dma8 ? 1 : 4;  // bytes per staged raw element
+    // 16-bit integer slots: 8-bit DMA rows in 256-sample time tiles; four
+    // alignment copies of >= 384 u16 elements, slots of <= 512 elements (span <= kS16Span)
+    const bool s16 = dma8 && TT == 256 && pu::knob("PU_SLOT16", p->opt_slot16) != 0;
+    const int64_t ncopies = s16 ? 4 : 2;
     const bool pack_cover = n < (int64_t(1) << 24);  // row bases fit 24 bits: covers above them
     // a stage's raw rows (DMA mode) and its slots share the LDS budget; a stage holds
     // whole groups.  The zero row (DMA mode, partial last group) sits at the end.
@@ -1494,14 +1743,18 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     auto raw_stride_of = [&](int64_t spread) {
         return dma8 ? (TT + spread + 1 + 3 + 255) / 256 * 256 : (TT + spread + 1 + 63) / 64 * 64;
     };
-    // slot copy: len = TT + span + 1 elements + 1 padding float (copy 1's element -1)
-    auto copy_of = [&](int64_t span) { return (TT + span + 2 + 63) / 64 * 64 * 4; };
+    // slot copy: len = TT + span + 1 elements + 1 padding float (copy 1's element -1);
+    // 16-bit slots: whole 128-element chunks, >= 3 of them, 2 elements of padding (copies
+    // 2 and 3 are written 4 bytes down)
+    auto copy_of = [&](int64_t span) {
+        return s16 ? std::max<int64_t>(384, (TT + span + 2 + 127) / 128 * 128) * 2 : (TT + span + 2 + 63) / 64 * 64 * 4;
+    };
     auto zero_bytes = [&](int64_t stride) { return partial ? ((stride + 64) * eb + 255) / 256 * 256 : 0; };
     auto raw_bytes = [&](int64_t chans, int64_t stride) { return dma ? (chans * stride * eb + 255) / 256 * 256 : 0; };
     // one group's rows, `slots` slots and the zero row fit the budget
     auto group_fits = [&](int64_t spread, int64_t slots, int64_t span) {
         const int64_t rs = raw_stride_of(spread);
-        return raw_bytes(G, rs) + slots * 2 * copy_of(span) + zero_bytes(rs) <= lds_cap;
+        return raw_bytes(G, rs) + slots * ncopies * copy_of(span) + zero_bytes(rs) <= lds_cap;
     };
     if (!group_fits(0, 1, 0)) return PU_EUNSUPPORTED;
 
@@ -1574,6 +1827,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
                     maxslots = std::max(maxslots, nxt[g].size());
                 }
                 if (!group_fits(sp, (int64_t)maxslots, spn)) break;
+                if (s16 && spn > kS16Span) break;  // a 16-bit slot holds <= 512 elements
                 for (int64_t c = 0; c < nchan; ++c) {
                     mn[c] = std::min(mn[c], S(j, c));
                     mx[c] = std::max(mx[c], S(j, c));
@@ -1607,7 +1861,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     for (int t = 0; t < ndt; ++t) {
         size_t maxslots = 0;
         for (int g = 0; g < ngroups; ++g) maxslots = std::max(maxslots, tslots[(size_t)t * ngroups + g].size());
-        if (raw_bytes(G, raw_stride) + (int64_t)maxslots * 2 * copy_of(span_t[t]) > stage_cap) {
+        if (raw_bytes(G, raw_stride) + (int64_t)maxslots * ncopies * copy_of(span_t[t]) > stage_cap) {
             pu::set_error("subband mode: a group does not fit the LDS budget");
             return PU_EUNSUPPORTED;
         }
@@ -1647,7 +1901,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
         const int64_t *smax = smax_t.data() + (size_t)t * nchan;
         const int64_t trials_run = (count[t] + D - 1) / D * D;  // active waves run all D trials
         adds_tile += trials_run * ngroups * TT;
-        lds_tile += trials_run * ngroups * TT * 4;  // sum: one window read per trial and group
+        lds_tile += trials_run * ngroups * TT * (s16 ? 2 : 4);  // sum: one window read per trial and group
         const int64_t row_len = TT + spread_t[t] + 1 + (dma8 ? 3 : 0);  // staged elements per row
         tiles[t] = i32x4{first[t], count[t], (int32_t)row_len, (int32_t)cb};
         if (dma)
@@ -1675,7 +1929,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
                     const int gs = (int)std::min<int64_t>(G, nchan - (int64_t)g_stop * G);
                     const int64_t ns = (int64_t)tslots[(size_t)t * ngroups + g_stop].size();
                     const int64_t rb = raw_bytes(ch + gs, raw_stride);
-                    if (g_stop > g && (rb + (u + ns) * 2 * cb > stage_cap || rb + prev_slots > stage_cap)) break;
+                    if (g_stop > g && (rb + (u + ns) * ncopies * cb > stage_cap || rb + prev_slots > stage_cap)) break;
                     u += ns;
                     ch += gs;
                     ++g_stop;
@@ -1684,7 +1938,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
                     pu::set_error("subband mode: consecutive stages do not fit the LDS budget");
                     return PU_EUNSUPPORTED;
                 }
-                prev_slots = u * 2 * cb;
+                prev_slots = u * ncopies * cb;
             }
             int g_end = g;
             while (g_end < g_stop) {
@@ -1693,11 +1947,15 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
                 const auto &sls = tslots[(size_t)t * ngroups + g_end];
                 slot_local[g_end] = used;
                 for (const auto &sl : sls) {
-                    const int64_t len = TT + (sl.hi - sl.lo) + 1;
+                    // 16-bit slots: len = the elements the windows read (the build's chunk count)
+                    const int64_t len = TT + (sl.hi - sl.lo) + (s16 ? 0 : 1);
                     adds_tile += len * gs;
-                    lds_tile += ((len + 63) / 64 * 64) * (dma ? eb * G + 8 : 8);  // build reads + 2 writes
+                    if (s16)  // chunks of 128: 2 G byte reads, 4 copies x 2 B
+                        lds_tile += std::max<int64_t>(3, (len + 127) / 128) * 128 * (G + 8);
+                    else
+                        lds_tile += ((len + 63) / 64 * 64) * (dma ? eb * G + 8 : 8);  // build reads + 2 writes
                     slotmeta.push_back((int32_t)len);
-                    slotmeta.push_back((int32_t)(zr + used * 2 * cb));
+                    slotmeta.push_back((int32_t)(zr + used * ncopies * cb));
                     slotmeta.push_back((int32_t)c0);
                     slotmeta.push_back(gs);
                     for (int k = 0; k < ms - 4; ++k) {
@@ -1723,7 +1981,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
             stages.push_back(i32x4{g, g_end, s_begin, (int32_t)(slotmeta.size() / ms)});
             tile_stages[t][1]++;
             if (dma) lds_tile += chans * ((row_len * eb + 255) / 256 * 256);  // DMA writes
-            slot_used = std::max(slot_used, zr + used * 2 * cb);
+            slot_used = std::max(slot_used, zr + used * ncopies * cb);
             for (int gg = g; gg < g_end; ++gg) slot_base[gg] = zr;
             max_stage_chans = std::max(max_stage_chans, chans);
             g = g_end;
@@ -1738,8 +1996,9 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
                     size_t si = 0;
                     while (sls[si].vid != v) ++si;
                     const int64_t rr = S(tr, (int64_t)gg * G) - sls[si].lo;
-                    r[d] = (uint32_t)(slot_base[gg] + (slot_local[gg] + (int64_t)si) * 2 * cb + (rr & 1) * cb +
-                                      (rr & ~int64_t(1)) * 4);
+                    // copy rr mod 2 (float32) / rr mod 4 (u16), the aligned element below rr
+                    r[d] = (uint32_t)(slot_base[gg] + (slot_local[gg] + (int64_t)si) * ncopies * cb +
+                                      (s16 ? (rr & 3) * cb + (rr & ~int64_t(3)) * 2 : (rr & 1) * cb + (rr & ~int64_t(1)) * 4));
                 }
             }
         }
@@ -1801,6 +2060,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     p->small_n = raw_stride + 2 > n ? 1 : 0;
     p->zero_len = zr ? (size_t)(((raw_stride + 64) * eb + 3) / 4) : 0;  // floats
     p->dma8 = dma8 ? 1 : 0;
+    p->slot16 = s16 ? 1 : 0;
     p->base_bits = pack_cover ? 24 : 31;
     p->slot_bytes = (size_t)slot_used;
     p->lds_bytes = (size_t)lds_total;
@@ -1857,6 +2117,7 @@ void reset_tables(pu_plan *p)
     keep.TT = p->TT;
     keep.ntt = p->ntt;
     keep.opt_u8_dma = p->opt_u8_dma;
+    keep.opt_slot16 = p->opt_slot16;
     keep.opt_dt_major = p->opt_dt_major;
     (void)hipFree(p->d_first);
     (void)hipFree(p->d_count);
@@ -2041,8 +2302,9 @@ int pu_plan_create_ex(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t 
     PU_REQUIRE(opts->shape >= -1 && opts->shape <= 2, "pu_plan_create_ex: shape %d not in {-1, 0, 1, 2}", opts->shape);
     PU_REQUIRE(opts->lds_budget_kb == 0 || (opts->lds_budget_kb >= 8 && opts->lds_budget_kb <= 160),
                "pu_plan_create_ex: lds_budget_kb %d not 0 or in [8, 160]", opts->lds_budget_kb);
-    PU_REQUIRE(opts->u8_dma >= -1 && opts->u8_dma <= 1 && opts->dt_major >= -1 && opts->dt_major <= 1,
-               "pu_plan_create_ex: u8_dma / dt_major must be -1, 0 or 1");
+    PU_REQUIRE(opts->u8_dma >= -1 && opts->u8_dma <= 1 && opts->dt_major >= -1 && opts->dt_major <= 1 &&
+                   opts->slot16 >= -1 && opts->slot16 <= 1,
+               "pu_plan_create_ex: u8_dma / dt_major / slot16 must be -1, 0 or 1");
     *out = nullptr;
     const int v = pick_variant(dtype, acc);
     PU_REQUIRE(v >= 0, "pu_plan_create: unsupported dtype %d", dtype);
@@ -2070,6 +2332,7 @@ int pu_plan_create_ex(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t 
     p->ntt = (int)((n + p->TT - 1) / p->TT);
     p->opt_u8_dma = opts->u8_dma < 0 ? 1 : opts->u8_dma;
     p->opt_dt_major = opts->dt_major;
+    p->opt_slot16 = opts->slot16 < 0 ? 1 : opts->slot16;
 
     // subband workgroup shape: 0 = wide (1 WG/CU), 1 = pair (2 WGs/CU), 2 = tall (256
     // trials x 256 samples, 1 WG/CU); -1 = the cost model's choice among wide and tall.
@@ -2118,6 +2381,7 @@ int pu_plan_create_ex(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t 
             q->TT = p->TT;
             q->ntt = p->ntt;
             q->opt_u8_dma = p->opt_u8_dma;
+            q->opt_slot16 = p->opt_slot16;
             q->opt_dt_major = p->opt_dt_major;
             return q;
         };

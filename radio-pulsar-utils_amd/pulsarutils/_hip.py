@@ -88,7 +88,8 @@ class HipBackendError(RuntimeError):
 class PlanOpts(ctypes.Structure):
     """``pu_plan_opts`` (include/pulsarutils_hip.h): the planner's explicit options."""
     _fields_ = [("group", ctypes.c_int32), ("shape", ctypes.c_int32), ("lds_budget_kb", ctypes.c_int32),
-                ("u8_dma", ctypes.c_int32), ("dt_major", ctypes.c_int32), ("reserved", ctypes.c_int32 * 3)]
+                ("u8_dma", ctypes.c_int32), ("dt_major", ctypes.c_int32), ("slot16", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 2)]
 
 
 SHAPES = {"wide": 0, "pair": 1, "tall": 2}
@@ -233,13 +234,14 @@ class Plan:
     """Owning wrapper of a ``pu_plan`` (dedispersion tiling + device metadata)."""
 
     def __init__(self, dtype_code_, acc, nchan, nsamples, shifts, group=0, shape=None, lds_budget_kb=0,
-                 u8_dma=None, dt_major=None):
+                 u8_dma=None, dt_major=None, slot16=None):
         """``group``: channels summed per group row (0 = library default, 1 = channel
         mode, 2/4/8); float64 accumulation always uses channel mode.  ``shape``: subband
         workgroup shape ("wide", "pair", "tall" or 0/1/2; None = the cost model's choice);
         ``lds_budget_kb``: LDS per workgroup (0 = default); ``u8_dma``: False builds 8-bit
         slots from global memory instead of LDS-DMA'd rows; ``dt_major``: work-item order
-        (None = automatic).  These are the planner's only inputs (pu_plan_create_ex): the
+        (None = automatic); ``slot16``: False keeps float32 slots where the planner would use
+        16-bit integer slots (8-bit DMA rows in 256-sample tiles).  These are the planner's only inputs (pu_plan_create_ex): the
         library reads no environment."""
         require_gpu()
         sh = np.ascontiguousarray(shifts, dtype=np.int64)
@@ -248,7 +250,8 @@ class Plan:
         ndm = sh.shape[0]
         opts = PlanOpts(group=int(group), shape=-1 if shape is None else int(SHAPES.get(shape, shape)),
                         lds_budget_kb=int(lds_budget_kb), u8_dma=-1 if u8_dma is None else int(bool(u8_dma)),
-                        dt_major=-1 if dt_major is None else int(bool(dt_major)))
+                        dt_major=-1 if dt_major is None else int(bool(dt_major)),
+                        slot16=-1 if slot16 is None else int(bool(slot16)))
         h = ctypes.c_void_p()
         check(lib().pu_plan_create_ex(ctypes.byref(h), dtype_code_, acc, nchan, nsamples,
                                       sh.ctypes.data_as(ctypes.c_void_p), ndm, ctypes.byref(opts)),

@@ -137,7 +137,7 @@ _PLAN_OPTS = threading.local()
 def planner_options(**opts):
     """Planner options for the plans the drop-in functions build in this thread (the
     keyword arguments of :class:`pulsarutils._hip.Plan`: ``group``, ``shape``,
-    ``lds_budget_kb``, ``u8_dma``, ``dt_major``).  The reference has no such knob; the
+    ``lds_budget_kb``, ``u8_dma``, ``dt_major``, ``slot16``).  The reference has no such knob; the
     defaults are the library's automatic choices.  Explicit and scoped: nothing is read
     from the environment."""
     old = getattr(_PLAN_OPTS, "opts", {})

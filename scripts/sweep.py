@@ -2,8 +2,9 @@
 
 Usage: python scripts/sweep.py [config]
   env PU_SWEEP="G:KB[:shape],..." selects (channel-group size, LDS budget KB, subband
-  workgroup shape 0 wide / 1 pair / 2 tall) variants, e.g. "1:64,4:160:0,4:80:1" (group
-  1 = channel mode).  PU_ROUNDS rounds.
+  workgroup shape 0 wide / 1 pair / 2 tall[, slot16 0/1]) variants, e.g.
+  "1:64,4:160:0,4:80:1" (group 1 = channel mode), "8:160:2:1,8:160:2:0" (8-bit C3: 16-bit vs
+  float32 slots).  PU_ROUNDS rounds, PU_TRIALS the first trials of the grid.
 Prints one line per (variant, round) and a median summary; the S/N of every trial
 is compared with the first variant's (float32 tolerance).
 """
@@ -30,7 +31,8 @@ sh = _hip.shift_table(cfg.nchan, dms, cfg.start_freq, cfg.bandwidth, cfg.tsamp)
 plans = {}
 for v in variants:
     plans[v] = _hip.Plan(_hip.dtype_code(x.dtype), _hip.PU_ACC_NATIVE, cfg.nchan, cfg.nsamples, sh, group=v[0],
-                         lds_budget_kb=v[1], shape=v[2] if len(v) > 2 else 0)
+                         lds_budget_kb=v[1], shape=v[2] if len(v) > 2 else 0,
+                         slot16=bool(v[3]) if len(v) > 3 else None)
     print("variant", v, plans[v].info, flush=True)
 ws = torch.empty(max(p.workspace_bytes for p in plans.values()), dtype=torch.uint8, device=x.device)
 res = {v: [] for v in plans}

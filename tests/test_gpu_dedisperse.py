@@ -590,3 +590,104 @@ def test_dedisperse_dm_tile_equals_full_plane(gpu, dt, acc, group):
     with pytest.raises(ValueError):
         _hip.check(_hip.lib().pu_plan_dedisperse_dm_tile(plan._h, _hip.ptr(xd), xd.stride(0), first.size,
                                                          _hip.ptr(full), full.stride(0), None), "dm_tile")
+
+
+def _slot16_pair(x, sh, **opts):
+    """The same trial grid planned with 16-bit integer slots and with float32 slots:
+    (plane16, plane32, search16, search32, info16, info32)."""
+    import torch
+    xd = _hip.to_device(x)
+    out = []
+    for s16 in (True, False):
+        plan = _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, x.shape[0], x.shape[1], sh, slot16=s16, **opts)
+        plane = plan.dedisperse(xd).cpu().numpy()
+        res = [v.cpu().numpy() for v in plan.search(xd)]
+        torch.cuda.synchronize()
+        out.append((plane, res, plan.info))
+    (p16, r16, i16), (p32, r32, i32) = out
+    return p16, p32, r16, r32, i16, i32
+
+
+@pytest.mark.parametrize("shape", ["tall", "pair"])
+@pytest.mark.parametrize("group", [2, 4, 8])
+def test_slot16_u8_matches_float_slots_and_oracle(gpu, shape, group):
+    """16-bit integer slots (8-bit input, 256-sample tiles): every plane row
+    bit-equal to the float64 oracle (integer sums < 2^24 are exact either way) and to the
+    float32-slot plan, and the search table (max, std, snr, rebin) bit-equal to the
+    float32-slot plan's - the epilogue sees the same float32 sums.  Ragged channel count
+    (a partial last group reads the zero row), N not a multiple of the tile, values up to
+    255."""
+    rng = np.random.default_rng(100 + group)
+    nchan, n = 203, 5000
+    x = rng.integers(0, 256, (nchan, n)).astype(np.uint8)
+    dms = np.linspace(0, 120, 300)
+    sh = _hip.shift_table(nchan, dms, 400., 100., 1e-3)
+    p16, p32, r16, r32, i16, i32 = _slot16_pair(x, sh, group=group, shape=shape)
+    assert i16["kernel"] == 3 and i32["kernel"] == 2, (i16, i32)
+    assert i16["group"] == group and i16["time_tile"] == 256
+    np.testing.assert_array_equal(p16, p32)
+    for k in range(0, sh.shape[0], 13):
+        np.testing.assert_array_equal(p16[k].astype(np.float64), oracle.dedisperse(x, sh[k]))
+    for a, b in zip(r16, r32):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_slot16_u8_full_scale_sums_and_flushes(gpu):
+    """All-255 input on 4096 channels: every window adds 8 x 255 per group, so the packed
+    u16 accumulators flush every 32 groups and the 256-unit halves carry the totals up to
+    4096 x 255 = 1044480 (< 2^24) - the plane equals the oracle bit for bit; a few rows of
+    noise on top make the series differ per trial."""
+    rng = np.random.default_rng(7)
+    nchan, n = 4096, 2048
+    x = np.full((nchan, n), 255, np.uint8)
+    x[rng.integers(0, nchan, 50), rng.integers(0, n, 50)] = 0
+    dms = np.linspace(0, 30, 40)
+    sh = _hip.shift_table(nchan, dms, 1200., 300., 64e-6)
+    p16, p32, r16, r32, i16, _ = _slot16_pair(x, sh, group=8, shape="tall")
+    assert i16["kernel"] == 3
+    np.testing.assert_array_equal(p16, p32)
+    for k in (0, 17, 39):
+        np.testing.assert_array_equal(p16[k].astype(np.float64), oracle.dedisperse(x, sh[k]))
+    for a, b in zip(r16, r32):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_slot16_u8_long_slots_c3_slice(gpu):
+    """C3's own channels and first 625 trials (the 8-GPU shard) at 2^16 samples: slot spans
+    up to ~150 samples, so some slots need the fourth 128-element build chunk (len > 384)
+    and the O stream's lane-63 hand-over between chunks - plane rows bit-equal to the
+    oracle, tables bit-equal to the float32-slot plan."""
+    from dataclasses import replace
+    from pulsarutils import synth
+    c = replace(CONFIGS["C3"], nsamples=1 << 16)
+    xd = synth.pulsar_filterbank_device(c)
+    x = xd.cpu().numpy()
+    del xd
+    dms = D.dedispersion_plan(c.nchan, c.dmmin, c.dmmax, c.start_freq, c.bandwidth, c.tsamp)[:625]
+    sh = _hip.shift_table(c.nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
+    p16, p32, r16, r32, i16, _ = _slot16_pair(x, sh)
+    assert i16["kernel"] == 3 and i16["group"] == 8, i16
+    np.testing.assert_array_equal(p16, p32)
+    for k in (0, 300, 624):
+        np.testing.assert_array_equal(p16[k].astype(np.float64), oracle.dedisperse(x, sh[k]))
+    for a, b in zip(r16, r32):
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("budget", [0, 64])
+def test_slot16_u8_wrapping_windows_and_small_budget(gpu, budget):
+    """Short series (windows wrap modulo N: the per-lane modular DMA) with large random
+    shifts, and a small LDS budget (one group per stage: the flush counter runs across
+    many stages) - planes equal the oracle, tables the float32-slot plan's."""
+    rng = np.random.default_rng(9)
+    nchan, n = 48, 1024
+    x = rng.integers(0, 256, (nchan, n)).astype(np.uint8)
+    sh = rng.integers(-20000, 20000, (70, nchan))
+    sh = np.sort(sh, axis=0)
+    p16, p32, r16, r32, i16, _ = _slot16_pair(x, sh, group=4, shape="tall", lds_budget_kb=budget)
+    assert i16["kernel"] == 3, i16
+    np.testing.assert_array_equal(p16, p32)
+    for k in range(0, 70, 9):
+        np.testing.assert_array_equal(p16[k].astype(np.float64), oracle.dedisperse(x, sh[k]))
+    for a, b in zip(r16, r32):
+        np.testing.assert_array_equal(a, b)
