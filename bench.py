@@ -121,6 +121,28 @@ def load_pmc(tag):
     return pmc, same
 
 
+def load_sq(tag, srcfile="csrc/dedisperse.hip"):
+    """The dominant kernel's SQ counter summary ``profiles/sq_<tag>.json`` (scripts/sq_json.py:
+    LDS-array cycles / CU cycles etc.) if it was collected from the kernel source this library
+    was built from, else None."""
+    path = os.path.join(REPO, "profiles", f"sq_{tag}.json")
+    try:
+        sq = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    return sq if sq.get("source_sha256") == _hip.source_hashes().get(srcfile) else None
+
+
+def sq_fields(sq, tag):
+    if not sq:
+        return {"lds_cycle_frac": None,
+                "lds_cycle_note": f"profiles/sq_{tag}.json absent or collected from another kernel source"}
+    return {"lds_cycle_frac": sq["lds_cycle_frac"], "lds_bank_conflict_frac": sq.get("lds_bank_conflict_frac"),
+            "insts_per_cu_cycle": sq.get("per_cu_cycle"),
+            "lds_cycle_source": f"profiles/sq_{tag}.json (SQ_LDS_IDX_ACTIVE / (256 CUs x GRBM_GUI_ACTIVE/8), "
+                                f"kernel {sq.get('kernel_ms_at_collection')} ms at collection)"}
+
+
 def knob_env():
     """Every PU_* / PULSARUTILS_* variable: tuning knobs that reshape the kernels or the
     library loaded (a bench line is only valid with none set)."""
@@ -218,7 +240,8 @@ def acc_f64_bench(x, dms, cfg, steps):
                         "peak": VALU_F64_ADD_PEAK_TFLOPS, "unit": "TFLOP/s (f64 adds)",
                         "frac": round(adds / (kms / 1e3) / 1e12 / VALU_F64_ADD_PEAK_TFLOPS, 4),
                         "lds_bytes_per_launch": info["lds_traffic"], "lds_achieved_TBps": round(lds, 2),
-                        "lds_peak_TBps": LDS_PEAK_TBPS, "lds_frac": round(lds / LDS_PEAK_TBPS, 4)},
+                        "lds_peak_TBps": LDS_PEAK_TBPS, "lds_frac": round(lds / LDS_PEAK_TBPS, 4),
+                        **sq_fields(load_sq("C2_f64", "csrc/dedisp_f64.hip"), "C2_f64")},
            "plan": {k: info[k] for k in ("dm_tiles", "time_tiles", "trials_per_tile", "time_tile", "chans_per_step",
                                          "lds_bytes")},
            "best_dm": float(dms[int(torch.argmax(outs[2]).item())]), "certify": plan.cert_info()}
@@ -556,10 +579,12 @@ def main():
                          "executed_tflops": round(info["exec_adds"] / (kernel_ms / 1e3) / 1e12, 3),
                          "lds_bytes_per_launch": info["lds_traffic"], "lds_achieved_TBps": round(lds, 2),
                          "lds_peak_TBps": LDS_PEAK_TBPS, "lds_frac": round(lds / LDS_PEAK_TBPS, 4),
+                         **sq_fields(load_sq(pmc_tag), pmc_tag),
                          "group": info["group"], "binding": "lds",
                          "binding_note": "frac is SURVEY 8(d)'s brute-force-equivalent adds / the f32 VALU-add "
                                          "peak; the subband decomposition executes group x fewer adds, and the "
-                                         "unit that binds it is the LDS array: lds_frac"})
+                                         "unit that binds it is the LDS array: lds_cycle_frac (counters: LDS-array "
+                                         "cycles / CU cycles), lds_frac (the planner's byte model)"})
 
     # N > 1, strong split: the same whole workload on rank 0's GPU alone (untimed by the
     # step; the other ranks wait), so the line carries its own one-GPU reference - the N = 1

@@ -394,7 +394,7 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 #define PU_WAIT1_CASE(N) asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(w) : : "memory");
 template <int N>
-__device__ __forceinline__ void wait_window1(double &w)
+__device__ __forceinline__ void wait_window1(u32x2 &w)
 {
     static_assert(N >= 0 && N <= 7, "lgkmcnt");
     if constexpr (N == 7) { PU_WAIT1_CASE(7) }
@@ -463,24 +463,32 @@ __device__ __forceinline__ uint32_t s16_chunk(uint32_t (&rb)[G][2], const uint32
     return s0 | (s1 << 16);
 }
 
-__device__ __forceinline__ void issue_window1(double &w, uint32_t addr)
+__device__ __forceinline__ void issue_window1(u32x2 &w, uint32_t addr)
 {
     asm volatile("ds_read_b64 %0, %1" : "=&v"(w) : "v"(addr) : "memory");
+}
+
+// A dword as a u16 pair.  (Through memcpy: hipcc 7.2 compiled __builtin_bit_cast(u16x2, v.y)
+// of an ext_vector element as the bits of v.x - the window's second dword was never added.)
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t d)
+{
+    u16x2 r;
+    __builtin_memcpy(&r, &d, 4);
+    return r;
 }
 
 // One group's contribution to the wave's D trials from 16-bit slots: one window read per
 // trial, issued A trials ahead of its two v_pk_add_u16.
 template <int D, int A, int I, typename RecT>
-__device__ __forceinline__ void trials16_step(u16x2 (&lo)[D][2], double (&w)[A + 1], const RecT &rec, uint32_t base)
+__device__ __forceinline__ void trials16_step(u16x2 (&lo)[D][2], u32x2 (&w)[A + 1], const RecT &rec, uint32_t base)
 {
     if constexpr (I < D) {
         if constexpr (I + A < D) issue_window1(w[(I + A) % (A + 1)], base + rec[I + A]);
         constexpr int ahead = D - 1 - I < A ? D - 1 - I : A;
-        double &wd = w[I % (A + 1)];
+        u32x2 &wd = w[I % (A + 1)];
         wait_window1<ahead>(wd);
-        const u32x2 v = __builtin_bit_cast(u32x2, wd);
-        lo[I][0] += __builtin_bit_cast(u16x2, v.x);
-        lo[I][1] += __builtin_bit_cast(u16x2, v.y);
+        lo[I][0] += as_u16x2(wd.x);
+        lo[I][1] += as_u16x2(wd.y);
         asm volatile("" : "+v"(lo[I][0]), "+v"(lo[I][1]));
         trials16_step<D, A, I + 1>(lo, w, rec, base);
     }
@@ -490,7 +498,7 @@ template <class C, typename RecT>
 __device__ __forceinline__ void group_trials16(u16x2 (&lo)[C::D][2], const RecT rec, uint32_t base)
 {
     constexpr int D = C::D, A = 5;
-    double w[A + 1];
+    u32x2 w[A + 1];
 #pragma unroll
     for (int d = 0; d < A && d < D; ++d) issue_window1(w[d], base + rec[d]);
     trials16_step<D, A, 0>(lo, w, rec, base);
@@ -1731,7 +1739,10 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     const int64_t eb = dma8 ? 1 : 4;  // bytes per staged raw element
     // 16-bit integer slots: 8-bit DMA rows in 256-sample time tiles; four
     // alignment copies of >= 384 u16 elements, slots of <= 512 elements (span <= kS16Span)
-    const bool s16 = dma8 && TT == 256 && pu::knob("PU_SLOT16", p->opt_slot16) != 0;
+    // G <= 4 only: G = 8 with 16-bit slots measured slower than with float32 slots (C3 625
+    // trials 140.6 vs 115.1 ms, 5000: 1055 vs 960; G = 4: 126.6 / 909.7 ms - DESIGN.md §4.1b,
+    // profiles/r06/experiments/slot16/)
+    const bool s16 = dma8 && TT == 256 && G <= 4 && pu::knob("PU_SLOT16", p->opt_slot16) != 0;
     const int64_t ncopies = s16 ? 4 : 2;
     const bool pack_cover = n < (int64_t(1) << 24);  // row bases fit 24 bits: covers above them
     // a stage's raw rows (DMA mode) and its slots share the LDS budget; a stage holds

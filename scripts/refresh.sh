@@ -7,7 +7,8 @@
 # script stops at the first step that fails.
 #   NOTEST=1: skip the test suite.  NOSMOKE=1: skip __graft_entry__.smoke().  SQ=1: SQ counter
 #   passes of the C3 625 shard.  MR=1: a 2-rank rehearsal of the N > 1 bench on this GPU.  PMC="C2 C5 C3 C3_625": the PMC configs.  CFGS=1: also
-#   bench lines for C1/C5/C3 (5000) / the C3 625-trial shard.
+#   bench lines for C1/C5/C3 (5000) / the C3 625-trial shard.  LDSC="C2 C3_625 C5 C2_f64": one SQ
+#   counter pass each (LDS-array cycles, bank conflicts, instruction counts) -> sq_<cfg>.json.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -31,6 +32,7 @@ args_of() {
     C5) echo "--config C5" ;;
     C3) echo "--config C3" ;;
     C3_625) echo "--config C3 --scaling strong --shard 8" ;;
+    C2_f64) echo "--config C2 --acc f64" ;;
     C1) echo "--config C1" ;;
   esac
 }
@@ -42,6 +44,16 @@ for cfg in ${PMC:-}; do
   timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $D/p1 -o run -- python3 bench.py $A --steps 1 --warmup 1 --no-cpu-baseline --no-clean --no-c3-strong > $D/p1.log 2>&1 || exit $?
   timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $D/p2 -o run -- python3 bench.py $A --steps 1 --warmup 1 --no-cpu-baseline --no-clean --no-c3-strong > $D/p2.log 2>&1 || exit $?
   python3 scripts/pmc_json.py $D $cfg $D/bench.json > $D/pmc_json.log 2>&1 || exit $?
+done
+for cfg in ${LDSC:-}; do
+  A=$(args_of $cfg)
+  D=$OUT/sq_$cfg
+  mkdir -p $D
+  PAT=dedisp_sub_kernel; SRC=csrc/dedisperse.hip
+  if [ $cfg = C2_f64 ]; then PAT=dedisp_f64_kernel; SRC=csrc/dedisp_f64.hip; fi
+  timeout -k 10 300 python3 -u bench.py $A --steps 3 --warmup 1 --no-cpu-baseline --no-clean --no-c3-strong --no-acc-f64 > $D/bench.json 2> $D/bench.err || exit $?
+  timeout -s KILL 300 rocprofv3 --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $D/p1 -o run -- python3 bench.py $A --steps 1 --warmup 1 --no-cpu-baseline --no-clean --no-c3-strong --no-acc-f64 > $D/p1.log 2>&1 || exit $?
+  python3 scripts/sq_json.py $D $cfg $D/bench.json $PAT $SRC > $D/sq_json.log 2>&1 || exit $?
 done
 if [ -n "$SQ" ]; then
   # SQ counter passes of the C3 625-trial shard (scalar vs vector issue) at this source
