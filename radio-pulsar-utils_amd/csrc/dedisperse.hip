@@ -386,11 +386,11 @@ __device__ __forceinline__ void group_trials(f32x2 (&acc)[C::D][C::J], const Rec
 // copies (copy s holds R[i + s] at element i), so every window - 256 samples, four per
 // lane - is ONE ds_read_b64 at an 8-byte-aligned address: half the sum's LDS reads of the
 // float32 slots (two ds_read_b64 per window).  Lane l owns samples 4 l .. 4 l + 3 of its D
-// trials in packed u16 accumulators `lo` (added by v_pk_add_u16: every add exact while
-// the total since the last flush stays < 2^16) and `hi` (units of 256): every <= F groups
-// (F G 255 + 255 < 2^16) `hi += lo >> 8, lo &= 255` - then hi 256 + lo is the exact
-// integer sum (< nchan 255 < 2^24), converted to float32 once per item.
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+// trials in packed u16 accumulators `lo` (every add exact while the total since the last
+// flush stays < 2^16) and `hi` (units of 256): every <= F groups (F G 255 + 255 < 2^16)
+// `hi += lo >> 8, lo &= 255` - then hi 256 + lo is the exact integer sum (< nchan 255 <
+// 2^24), converted to float32 once per item.  The u16 pairs are added as plain 32-bit words
+// (v_add_u32): each half stays below 2^16, so no carry crosses into the high half.
 
 #define PU_WAIT1_CASE(N) asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(w) : : "memory");
 template <int N>
@@ -423,44 +423,63 @@ __device__ __forceinline__ void wait_lgkm(uint32_t &v)
 
 // 16-bit slot build, one chunk of 128 elements: lane l's two elements 128 c + 2 l (+ 1) as
 // the byte sums of the G channels (addresses ad[q], reads rb in flight).
-template <int G, int C>
-__device__ __forceinline__ void s16_issue(uint32_t (&rb)[G][2], const uint32_t (&ad)[G])
+// 16-bit slot build, P = 8 / G chunks of 128 elements in flight (2 G P = 16 byte reads,
+// all the lgkmcnt field can count): register set C % P holds chunk C's reads.
+template <int G, int P, int C>
+__device__ __forceinline__ void s16_issue(uint32_t (&rb)[P][G][2], const uint32_t (&ad)[G])
 {
 #pragma unroll
     for (int q = 0; q < G; ++q) {
-        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(rb[q][0]) : "v"(ad[q]), "i"(128 * C) : "memory");
-        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(rb[q][1]) : "v"(ad[q]), "i"(128 * C + 1) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(rb[C % P][q][0]) : "v"(ad[q]), "i"(128 * C) : "memory");
+        asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(rb[C % P][q][1]) : "v"(ad[q]), "i"(128 * C + 1) : "memory");
+    }
+}
+
+template <int G, int P, int C, int NCH>
+__device__ __forceinline__ void s16_issue_first(uint32_t (&rb)[P][G][2], const uint32_t (&ad)[G])
+{
+    if constexpr (C < P && C < NCH) {
+        s16_issue<G, P, C>(rb, ad);
+        s16_issue_first<G, P, C + 1, NCH>(rb, ad);
     }
 }
 
 // Read i of chunk C (channel i / 2, byte i % 2): wait until it landed - the reads complete
-// in issue order, so it is the oldest outstanding when the 2 G - 1 later reads of this chunk
-// and (NEXT) the i already re-issued for chunk C + 1 may still be in flight: lgkmcnt(2 G -
-// 1), or 2 G - 1 - i for the last chunk (an outstanding scalar load only lengthens the
-// wait) - add it, and (NEXT) re-issue its register for chunk C + 1.
-template <int G, int C, bool NEXT, int I>
-__device__ __forceinline__ void s16_step(uint32_t (&rb)[G][2], const uint32_t (&ad)[G], uint32_t &s0, uint32_t &s1)
+// in issue order, so the wait allows every read issued after it to be outstanding: the rest
+// of chunk C, the chunks after C already issued and (NEXT) the i already re-issued for chunk
+// C + P: lgkmcnt(2 G P - 1) in steady state (an outstanding scalar load only lengthens the
+// wait) - add it, and (NEXT) re-issue its register for chunk C + P.
+template <int G, int P, int C, int NCH, int I>
+__device__ __forceinline__ void s16_step(uint32_t (&rb)[P][G][2], const uint32_t (&ad)[G], uint32_t &s0, uint32_t &s1)
 {
     if constexpr (I < 2 * G) {
         constexpr int q = I >> 1, e = I & 1;
-        static_assert(2 * G - 1 <= 15, "lgkmcnt");
-        wait_lgkm<NEXT ? 2 * G - 1 : 2 * G - 1 - I>(rb[q][e]);
+        constexpr bool NEXT = C + P < NCH;
+        constexpr int L = (C + P <= NCH ? P : NCH - C) - 1;  // later chunks already in flight
+        constexpr int N = NEXT ? 2 * G * P - 1 : 2 * G - 1 - I + 2 * G * L;
+        static_assert(N >= 0 && N <= 15, "lgkmcnt");
+        uint32_t &r = rb[C % P][q][e];
+        wait_lgkm<N>(r);
         if constexpr (e == 0)
-            s0 += rb[q][e];
+            s0 += r;
         else
-            s1 += rb[q][e];
+            s1 += r;
         if constexpr (NEXT)
-            asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(rb[q][e]) : "v"(ad[q]), "i"(128 * (C + 1) + e) : "memory");
-        s16_step<G, C, NEXT, I + 1>(rb, ad, s0, s1);
+            asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(r) : "v"(ad[q]), "i"(128 * (C + P) + e) : "memory");
+        s16_step<G, P, C, NCH, I + 1>(rb, ad, s0, s1);
     }
 }
 
-template <int G, int C, bool NEXT>
-__device__ __forceinline__ uint32_t s16_chunk(uint32_t (&rb)[G][2], const uint32_t (&ad)[G])
+// chunks C .. NCH - 1: e[c] = lane l's elements 128 c + 2 l (+ 1) as a u16 pair
+template <int G, int P, int C, int NCH>
+__device__ __forceinline__ void s16_run(uint32_t (&rb)[P][G][2], const uint32_t (&ad)[G], uint32_t (&e)[4])
 {
-    uint32_t s0 = 0, s1 = 0;
-    s16_step<G, C, NEXT, 0>(rb, ad, s0, s1);
-    return s0 | (s1 << 16);
+    if constexpr (C < NCH) {
+        uint32_t s0 = 0, s1 = 0;
+        s16_step<G, P, C, NCH, 0>(rb, ad, s0, s1);
+        e[C] = s0 | (s1 << 16);
+        s16_run<G, P, C + 1, NCH>(rb, ad, e);
+    }
 }
 
 __device__ __forceinline__ void issue_window1(u32x2 &w, uint32_t addr)
@@ -468,34 +487,25 @@ __device__ __forceinline__ void issue_window1(u32x2 &w, uint32_t addr)
     asm volatile("ds_read_b64 %0, %1" : "=&v"(w) : "v"(addr) : "memory");
 }
 
-// A dword as a u16 pair.  (Through memcpy: hipcc 7.2 compiled __builtin_bit_cast(u16x2, v.y)
-// of an ext_vector element as the bits of v.x - the window's second dword was never added.)
-__device__ __forceinline__ u16x2 as_u16x2(uint32_t d)
-{
-    u16x2 r;
-    __builtin_memcpy(&r, &d, 4);
-    return r;
-}
-
 // One group's contribution to the wave's D trials from 16-bit slots: one window read per
 // trial, issued A trials ahead of its two v_pk_add_u16.
 template <int D, int A, int I, typename RecT>
-__device__ __forceinline__ void trials16_step(u16x2 (&lo)[D][2], u32x2 (&w)[A + 1], const RecT &rec, uint32_t base)
+__device__ __forceinline__ void trials16_step(uint32_t (&lo)[D][2], u32x2 (&w)[A + 1], const RecT &rec, uint32_t base)
 {
     if constexpr (I < D) {
         if constexpr (I + A < D) issue_window1(w[(I + A) % (A + 1)], base + rec[I + A]);
         constexpr int ahead = D - 1 - I < A ? D - 1 - I : A;
         u32x2 &wd = w[I % (A + 1)];
         wait_window1<ahead>(wd);
-        lo[I][0] += as_u16x2(wd.x);
-        lo[I][1] += as_u16x2(wd.y);
+        lo[I][0] += wd.x;  // two u16 sums per dword: no carry crosses (each half < 2^16)
+        lo[I][1] += wd.y;
         asm volatile("" : "+v"(lo[I][0]), "+v"(lo[I][1]));
         trials16_step<D, A, I + 1>(lo, w, rec, base);
     }
 }
 
 template <class C, typename RecT>
-__device__ __forceinline__ void group_trials16(u16x2 (&lo)[C::D][2], const RecT rec, uint32_t base)
+__device__ __forceinline__ void group_trials16(uint32_t (&lo)[C::D][2], const RecT rec, uint32_t base)
 {
     constexpr int D = C::D, A = 5;
     u32x2 w[A + 1];
@@ -504,16 +514,17 @@ __device__ __forceinline__ void group_trials16(u16x2 (&lo)[C::D][2], const RecT 
     trials16_step<D, A, 0>(lo, w, rec, base);
 }
 
-// hi += lo >> 8, lo &= 255 (exact: lo < 2^16; hi counts 256s, < nchan < 2^16)
+// per 16-bit half: hi += lo >> 8, lo &= 255 (exact: lo < 2^16; hi counts 256s, < nchan < 2^16,
+// so neither 32-bit add carries across the halves)
 template <int D>
-__device__ __forceinline__ void flush16(u16x2 (&lo)[D][2], u16x2 (&hi)[D][2])
+__device__ __forceinline__ void flush16(uint32_t (&lo)[D][2], uint32_t (&hi)[D][2])
 {
 #pragma unroll
     for (int d = 0; d < D; ++d)
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-            hi[d][k] += lo[d][k] >> (u16x2){8, 8};
-            lo[d][k] &= (u16x2){0xff, 0xff};
+            hi[d][k] += (lo[d][k] >> 8) & 0x00ff00ffu;
+            lo[d][k] &= 0x00ff00ffu;
         }
 }
 
@@ -521,7 +532,7 @@ __device__ __forceinline__ void flush16(u16x2 (&lo)[D][2], u16x2 (&hi)[D][2])
 // e), which the epilogues and write_outputs take: sample 128 j + 2 l + e lives in lane
 // 32 j + l / 2, element 2 (l & 1) + e - four ds_bpermute per (trial, j) and a select.
 template <int D>
-__device__ __forceinline__ void s16_to_pairs(const u16x2 (&lo)[D][2], const u16x2 (&hi)[D][2], f32x2 (&acc)[D][2],
+__device__ __forceinline__ void s16_to_pairs(const uint32_t (&lo)[D][2], const uint32_t (&hi)[D][2], f32x2 (&acc)[D][2],
                                              int lane)
 {
     const bool odd = lane & 1;
@@ -530,8 +541,8 @@ __device__ __forceinline__ void s16_to_pairs(const u16x2 (&lo)[D][2], const u16x
         float v[4];
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-            v[2 * k] = (float)((uint32_t)hi[d][k].x * 256u + (uint32_t)lo[d][k].x);
-            v[2 * k + 1] = (float)((uint32_t)hi[d][k].y * 256u + (uint32_t)lo[d][k].y);
+            v[2 * k] = (float)((hi[d][k] & 0xffffu) * 256u + (lo[d][k] & 0xffffu));
+            v[2 * k + 1] = (float)((hi[d][k] >> 16) * 256u + (lo[d][k] >> 16));
         }
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -630,12 +641,12 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
     }
     // 16-bit slots: packed u16 accumulators, flushed every <= F16 groups (see flush16)
     constexpr int F16 = (65535 - 255) / (G * 255);
-    u16x2 lo16[S16 ? D : 1][2], hi16[S16 ? D : 1][2];
+    uint32_t lo16[S16 ? D : 1][2], hi16[S16 ? D : 1][2];  // u16 pairs: (sample 4 l + 2 k, + 1)
     if constexpr (S16) {
 #pragma unroll
         for (int d = 0; d < D; ++d)
 #pragma unroll
-            for (int k = 0; k < 2; ++k) lo16[d][k] = hi16[d][k] = u16x2{0, 0};
+            for (int k = 0; k < 2; ++k) lo16[d][k] = hi16[d][k] = 0u;
     }
     int gc16 = 0;  // groups added since the last flush
 
@@ -818,8 +829,9 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
     // with the next lane's low half (DPP wave_shl:1; lane 63 takes chunk u + 1's lane 0 by
     // wave_rol:1).  Stores by ds_write_addtid_b32: E_u to copy 0 and, 4 bytes down, copy 2;
     // O_u to copy 1 and, 4 bytes down, copy 3 (element i of copy s is R[i + s]).  Chunks
-    // 0-2 always (the planner's copies hold >= 384 elements, len <= 512), chunk 3 when len >
-    // 384; reads of chunk c + 1 in flight while chunk c is summed.
+    // 0-2 always (len <= 512; a chunk past the copy's end stores only its lanes inside it),
+    // chunk 3 when len > 384; the reads of the next 8 / G chunks in flight while a chunk is
+    // summed.
     auto slot16 = [&](const meta_t &m) {
         const bool four = m[0] > 384;
         auto odd = [&](uint32_t e, uint32_t enext) {  // (R[2k + 1], R[2k + 2]) of lane k
@@ -828,32 +840,37 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
             return __builtin_amdgcn_alignbit(y, e, 16);
         };
         // per channel the lane's byte address; 2 G byte reads per chunk (ds_read_u8 in inline
-        // asm: the order kept by s16_chunk holds ~15 in flight in 16 registers - each value is
-        // added, then its register takes the next chunk's read of the same channel and byte)
+        // asm: the order kept by s16_run holds ~15 in flight in 16 registers - each value is
+        // added, then its register takes the read of chunk c + 8 / G, same channel and byte)
         uint32_t ad[G];
 #pragma unroll
         for (int q = 0; q < G; ++q) ad[q] = smem_addr + (uint32_t)m[4 + q] + 2u * (uint32_t)lane;
-        uint32_t rb[G][2];
-        s16_issue<G, 0>(rb, ad);
-        const uint32_t e0 = s16_chunk<G, 0, true>(rb, ad);
-        const uint32_t e1 = s16_chunk<G, 1, true>(rb, ad);
-        uint32_t e2, e3 = 0;
+        constexpr int P = 8 / G;
+        uint32_t rb[P][G][2];
+        uint32_t e[4] = {0u, 0u, 0u, 0u};
         if (four) {
-            e2 = s16_chunk<G, 2, true>(rb, ad);
-            e3 = s16_chunk<G, 3, false>(rb, ad);
+            s16_issue_first<G, P, 0, 4>(rb, ad);
+            s16_run<G, P, 0, 4>(rb, ad, e);
         } else {
-            e2 = s16_chunk<G, 2, false>(rb, ad);
+            s16_issue_first<G, P, 0, 3>(rb, ad);
+            s16_run<G, P, 0, 3>(rb, ad, e);
         }
+        const uint32_t e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
         uint32_t o0 = odd(e0, e1), o1 = odd(e1, e2), o2 = odd(e2, e3), o3 = four ? odd(e3, e3) : 0u;
         asm volatile("" : "+v"(o0), "+v"(o1), "+v"(o2), "+v"(o3));
         const uint32_t c0 = lds_base + (uint32_t)m[1];
         const uint32_t cbu = (uint32_t)copy_bytes;
+        // a chunk reaching past its copy (copies hold TT + span + 2 elements rounded to 64)
+        // stores only its lanes inside it (elements 128 c + 2 l <= copy - 2; copies 2 / 3 give
+        // up their last dword, beyond every window)
+        const bool fit2 = 768u <= cbu, fit3 = 1024u <= cbu;
+        const bool in2 = 512 + 4 * lane <= (int)cbu - 4, in3 = 768 + 4 * lane <= (int)cbu - 4;
         auto store = [&](uint32_t base, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
             asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(base) : "memory");
             asm volatile("ds_write_addtid_b32 %0 offset:0" : : "v"(v0) : "memory");
             asm volatile("ds_write_addtid_b32 %0 offset:256" : : "v"(v1) : "memory");
-            asm volatile("ds_write_addtid_b32 %0 offset:512" : : "v"(v2) : "memory");
-            if (four) asm volatile("ds_write_addtid_b32 %0 offset:768" : : "v"(v3) : "memory");
+            if (fit2 || in2) asm volatile("ds_write_addtid_b32 %0 offset:512" : : "v"(v2) : "memory");
+            if (four && (fit3 || in3)) asm volatile("ds_write_addtid_b32 %0 offset:768" : : "v"(v3) : "memory");
         };
         store(c0, e0, e1, e2, e3);
         store(c0 + 2u * cbu - 4u, e0, e1, e2, e3);
@@ -1266,7 +1283,7 @@ struct pu_plan {
     std::vector<int32_t> tile_first, tile_count;  // DM tiles in launch order (pu_plan_dm_tiles)
     int64_t nstages = 0;
     int dt_major = 0;  // subband item order (SubArgs::dt_major)
-    int opt_u8_dma = -1, opt_dt_major = -1, opt_slot16 = 1;  // pu_plan_opts (planner inputs)
+    int opt_u8_dma = -1, opt_dt_major = -1, opt_slot16 = -1;  // pu_plan_opts (planner inputs)
     i32x4 *d_tiles = nullptr, *d_stages = nullptr;
     i32x2 *d_tile_stages = nullptr;
     int32_t *d_slots = nullptr;
@@ -1742,7 +1759,8 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     // G <= 4 only: G = 8 with 16-bit slots measured slower than with float32 slots (C3 625
     // trials 140.6 vs 115.1 ms, 5000: 1055 vs 960; G = 4: 126.6 / 909.7 ms - DESIGN.md §4.1b,
     // profiles/r06/experiments/slot16/)
-    const bool s16 = dma8 && TT == 256 && G <= 4 && pu::knob("PU_SLOT16", p->opt_slot16) != 0;
+    const int s16opt = pu::knob("PU_SLOT16", p->opt_slot16);  // -1 auto (G <= 4), 0 off, 1 any G
+    const bool s16 = dma8 && TT == 256 && (s16opt > 0 || (s16opt < 0 && G <= 4));
     const int64_t ncopies = s16 ? 4 : 2;
     const bool pack_cover = n < (int64_t(1) << 24);  // row bases fit 24 bits: covers above them
     // a stage's raw rows (DMA mode) and its slots share the LDS budget; a stage holds
@@ -1755,11 +1773,8 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
         return dma8 ? (TT + spread + 1 + 3 + 255) / 256 * 256 : (TT + spread + 1 + 63) / 64 * 64;
     };
     // slot copy: len = TT + span + 1 elements + 1 padding float (copy 1's element -1);
-    // 16-bit slots: whole 128-element chunks, >= 3 of them, 2 elements of padding (copies
-    // 2 and 3 are written 4 bytes down)
-    auto copy_of = [&](int64_t span) {
-        return s16 ? std::max<int64_t>(384, (TT + span + 2 + 127) / 128 * 128) * 2 : (TT + span + 2 + 63) / 64 * 64 * 4;
-    };
+    // 16-bit slots: TT + span + 2 u16 (copies 2 and 3 are written 4 bytes down), 64-rounded
+    auto copy_of = [&](int64_t span) { return (TT + span + 2 + 63) / 64 * 64 * (s16 ? 2 : 4); };
     auto zero_bytes = [&](int64_t stride) { return partial ? ((stride + 64) * eb + 255) / 256 * 256 : 0; };
     auto raw_bytes = [&](int64_t chans, int64_t stride) { return dma ? (chans * stride * eb + 255) / 256 * 256 : 0; };
     // one group's rows, `slots` slots and the zero row fit the budget
@@ -2343,7 +2358,7 @@ int pu_plan_create_ex(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t 
     p->ntt = (int)((n + p->TT - 1) / p->TT);
     p->opt_u8_dma = opts->u8_dma < 0 ? 1 : opts->u8_dma;
     p->opt_dt_major = opts->dt_major;
-    p->opt_slot16 = opts->slot16 < 0 ? 1 : opts->slot16;
+    p->opt_slot16 = opts->slot16;
 
     // subband workgroup shape: 0 = wide (1 WG/CU), 1 = pair (2 WGs/CU), 2 = tall (256
     // trials x 256 samples, 1 WG/CU); -1 = the cost model's choice among wide and tall.

@@ -622,7 +622,7 @@ def _slot16_pair(x, sh, **opts):
 
 
 @pytest.mark.parametrize("shape", ["tall", "pair"])
-@pytest.mark.parametrize("group", [2, 4])
+@pytest.mark.parametrize("group", [2, 4, 8])
 def test_slot16_u8_matches_float_slots_and_oracle(gpu, shape, group):
     """16-bit integer slots (8-bit input, 256-sample tiles): every plane row
     bit-equal to the float64 oracle (integer sums < 2^24 are exact either way) and to the
@@ -707,11 +707,12 @@ def test_slot16_u8_wrapping_windows_and_small_budget(gpu, budget):
 
 
 def test_slot16_declined_for_group_8(gpu):
-    """The planner keeps float32 slots for G = 8 (16-bit slots measured slower there:
-    DESIGN.md §4.1b), whatever slot16 says."""
+    """By default the planner keeps float32 slots for G = 8 (16-bit slots measured slower
+    there: DESIGN.md §4.1b) and uses 16-bit slots for G <= 4; slot16=True forces them for
+    any group size, slot16=False never."""
     x = np.zeros((64, 4096), np.uint8)
     sh = _hip.shift_table(64, np.linspace(0, 50, 40), 400., 100., 1e-3)
-    plan = _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, 64, 4096, sh, group=8, shape="tall", slot16=True)
-    assert plan.info["group"] == 8 and plan.info["kernel"] == 2, plan.info
-    plan = _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, 64, 4096, sh, group=4, shape="tall", slot16=True)
-    assert plan.info["kernel"] == 3, plan.info
+    mk = lambda g, s16: _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, 64, 4096, sh, group=g, shape="tall",
+                                   slot16=s16).info
+    assert mk(8, None)["kernel"] == 2 and mk(4, None)["kernel"] == 3 and mk(2, None)["kernel"] == 3
+    assert mk(8, True)["kernel"] == 3 and mk(4, False)["kernel"] == 2
