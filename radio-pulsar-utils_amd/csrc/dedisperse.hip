@@ -1280,6 +1280,7 @@ struct pu_plan {
     int base_bits = 31;  // subband DMA row words: base bits (24: per-channel cover above them)
     size_t slot_bytes = 0, zero_len = 0;
     int64_t exec_adds = 0, lds_traffic = 0;  // per launch (measurement: bench.py roofline)
+    int64_t cost_windows16 = 0;  // 16-bit-slot windows per launch (the cost model's extra term)
     std::vector<int32_t> tile_first, tile_count;  // DM tiles in launch order (pu_plan_dm_tiles)
     int64_t nstages = 0;
     int dt_major = 0;  // subband item order (SubArgs::dt_major)
@@ -1919,6 +1920,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     };
     int64_t slot_used = 0, max_stage_chans = 0;
     int64_t adds_tile = 0, lds_tile = 0;  // per time tile, summed over DM tiles
+    int64_t win16_tile = 0;               // 16-bit-slot windows per time tile
     std::vector<double> tile_cost((size_t)ndt);  // per DM tile: LDS bytes + stage overhead (cost model)
     for (int t = 0; t < ndt; ++t) {
         const int64_t lds_before = lds_tile;
@@ -1928,6 +1930,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
         const int64_t trials_run = (count[t] + D - 1) / D * D;  // active waves run all D trials
         adds_tile += trials_run * ngroups * TT;
         lds_tile += trials_run * ngroups * TT * (s16 ? 2 : 4);  // sum: one window read per trial and group
+        if (s16) win16_tile += trials_run * ngroups;
         const int64_t row_len = TT + spread_t[t] + 1 + (dma8 ? 3 : 0);  // staged elements per row
         tiles[t] = i32x4{first[t], count[t], (int32_t)row_len, (int32_t)cb};
         if (dma)
@@ -2095,6 +2098,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     p->dt_major = dt_major ? 1 : 0;
     p->exec_adds = adds_tile * ntt;
     p->lds_traffic = lds_tile * ntt;
+    p->cost_windows16 = win16_tile * ntt;
     // host tables only: the caller uploads the plan it keeps (upload_sub), so comparing
     // candidate group sizes costs no device memory
     p->tile_first.resize((size_t)ndt);
@@ -2394,7 +2398,14 @@ int pu_plan_create_ex(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t 
         // stages cost more than that at C2 (22.7 vs 18.4 ms) and C5.  Only the winner's
         // tables are uploaded.  A candidate that does not fit (PU_EUNSUPPORTED) is not
         // viable; any other error is returned as is.
-        auto cost = [](const pu_plan *q) { return (double)q->lds_traffic + 3.0e6 * (double)q->nstages * q->ntt; };
+        // Round 6: a 16-bit-slot window costs more than its 512 LDS bytes say (its sum is not
+        // LDS-bound: the u16 G = 4 plan lost 6 % to float32 G = 8 at C3's 625-trial shard
+        // and won 10 % at its 5000 trials, which the byte model alone ranks the same way at
+        // both): + 200 B-equivalent per window, the middle of the (88, 389) the two
+        // measurements allow.
+        auto cost = [](const pu_plan *q) {
+            return (double)q->lds_traffic + 3.0e6 * (double)q->nstages * q->ntt + 200.0 * (double)q->cost_windows16;
+        };
         auto fresh = [&]() {
             pu_plan *q = new pu_plan();
             q->dtype = p->dtype;

@@ -716,3 +716,16 @@ def test_slot16_declined_for_group_8(gpu):
                                    slot16=s16).info
     assert mk(8, None)["kernel"] == 2 and mk(4, None)["kernel"] == 3 and mk(2, None)["kernel"] == 3
     assert mk(8, True)["kernel"] == 3 and mk(4, False)["kernel"] == 2
+
+
+def test_c3_plan_choice_shard_and_full(gpu):
+    """The planner's cost model at C3's two measured operating points:
+    the 625-trial shard of the 8-GPU split keeps tall G = 8 with float32 slots (114.2 vs
+    121.3 ms for 16-bit G = 4), the whole 5000-trial grid takes tall G = 4 with 16-bit slots
+    (858 vs 954 ms)."""
+    c = CONFIGS["C3"]
+    dms = D.dedispersion_plan(c.nchan, c.dmmin, c.dmmax, c.start_freq, c.bandwidth, c.tsamp)
+    for ntr, group, kernel in ((625, 8, 2), (5000, 4, 3)):
+        sh = _hip.shift_table(c.nchan, dms[:ntr], c.start_freq, c.bandwidth, c.tsamp)
+        info = _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, c.nchan, c.nsamples, sh).info
+        assert (info["group"], info["kernel"], info["trials_per_tile"]) == (group, kernel, 256), (ntr, info)
