@@ -9,6 +9,7 @@
 #   passes of the C3 625 shard.  MR=1: a 2-rank rehearsal of the N > 1 bench on this GPU.  PMC="C2 C5 C3 C3_625": the PMC configs.  CFGS=1: also
 #   bench lines for C1/C5/C3 (5000) / the C3 625-trial shard.  LDSC="C2 C3_625 C5 C2_f64": one SQ
 #   counter pass each (LDS-array cycles, bank conflicts, instruction counts) -> sq_<cfg>.json.
+#   UNPACK=1: the multi-GPU receivers' unpack-copy cost at C3's shape (scripts/unpack_cost.py).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -71,6 +72,10 @@ if [ -n "$MR" ]; then
   timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
     --master-port 29533 bench.py --gpus 2 --config C5 --dist-backend gloo --steps 2 --warmup 1 --bcast-chunks 4 \
     > $OUT/mr_bench_c5.json 2> $OUT/mr_bench_c5.err || exit $?
+fi
+if [ -n "$UNPACK" ]; then
+  # the receivers' staging -> strided copy of the N > 1 step at C3's shape
+  timeout -k 10 300 python3 -u scripts/unpack_cost.py 8 > $OUT/unpack_cost.json 2> $OUT/unpack_cost.err || exit $?
 fi
 if [ -n "$CFGS" ]; then
   for cfg in C1 C5 C3 C3_625; do
