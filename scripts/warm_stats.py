@@ -5,7 +5,8 @@
 rocprofv3 --stats averages every launch, the first (cold: code object load, caches and
 TLB empty) included.  This drops the first K launches of each kernel (default 1: the
 bench's warm-up runs every kernel at least once before the timed steps) and prints
-Name, Calls, AverageNs, MinNs, MaxNs, StdDevNs, SkippedCalls, ColdFirstNs.
+Name, Calls, AverageNs, MedianNs, MinNs, MaxNs, StdDevNs, SkippedCalls, ColdFirstNs (the median
+beside the mean: one slow launch on a shared box moves the mean, not the median).
 """
 import csv
 import glob
@@ -32,14 +33,17 @@ def main():
                 t0, t1 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
                 launches.setdefault(name, []).append((t0, t1 - t0))
     w = csv.writer(sys.stdout)
-    w.writerow(["Name", "Calls", "AverageNs", "MinNs", "MaxNs", "StdDevNs", "SkippedCalls", "ColdFirstNs"])
+    w.writerow(["Name", "Calls", "AverageNs", "MedianNs", "MinNs", "MaxNs", "StdDevNs", "SkippedCalls", "ColdFirstNs"])
     rows = []
     for name, ls in launches.items():
         ls.sort()
         warm = [d for _, d in ls[skip:]] or [d for _, d in ls]
         avg = sum(warm) / len(warm)
         sd = math.sqrt(sum((d - avg) ** 2 for d in warm) / len(warm))
-        rows.append((sum(warm), [name, len(warm), f"{avg:.1f}", min(warm), max(warm), f"{sd:.1f}",
+        srt = sorted(warm)
+        m = len(srt) // 2
+        med = srt[m] if len(srt) % 2 else (srt[m - 1] + srt[m]) / 2
+        rows.append((sum(warm), [name, len(warm), f"{avg:.1f}", f"{med:.1f}", min(warm), max(warm), f"{sd:.1f}",
                                  len(ls) - len(warm), ls[0][1]]))
     for _, row in sorted(rows, key=lambda x: -x[0]):
         w.writerow(row)
