@@ -421,6 +421,17 @@ __device__ __forceinline__ void wait_lgkm(uint32_t &v)
 }
 #undef PU_WAITV_CASE
 
+#define PU_WAIT2_CASE(N) else if constexpr (N0 == N) asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(v) : : "memory");
+template <int N0>
+__device__ __forceinline__ void wait_lgkm2(u32x2 &v)
+{
+    static_assert(N0 >= 0 && N0 <= 7, "lgkmcnt");
+    if constexpr (N0 == 0) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v) : : "memory");
+    PU_WAIT2_CASE(1) PU_WAIT2_CASE(2) PU_WAIT2_CASE(3) PU_WAIT2_CASE(4) PU_WAIT2_CASE(5) PU_WAIT2_CASE(6)
+    PU_WAIT2_CASE(7)
+}
+#undef PU_WAIT2_CASE
+
 // 16-bit slot build, one chunk of 128 elements: lane l's two elements 128 c + 2 l (+ 1) as
 // the byte sums of the G channels (addresses ad[q], reads rb in flight).
 // 16-bit slot build, P = 8 / G chunks of 128 elements in flight (2 G P = 16 byte reads,
@@ -432,6 +443,49 @@ __device__ __forceinline__ void s16_issue(uint32_t (&rb)[P][G][2], const uint32_
     for (int q = 0; q < G; ++q) {
         asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(rb[C % P][q][0]) : "v"(ad[q]), "i"(128 * C) : "memory");
         asm volatile("ds_read_u8 %0, %1 offset:%2" : "=v"(rb[C % P][q][1]) : "v"(ad[q]), "i"(128 * C + 1) : "memory");
+    }
+}
+
+template <int G, int Q>
+__device__ __forceinline__ void s16_quad_step(u32x2 (&d)[G], const uint32_t (&src)[G], uint32_t &acc02, uint32_t &acc13)
+{
+    if constexpr (Q < G) {
+        wait_lgkm2<G - 1 - Q>(d[Q]);
+        const uint32_t t = __builtin_amdgcn_alignbyte(d[Q].y, d[Q].x, src[Q]);  // bytes src .. src + 3
+        acc02 += t & 0x00ff00ffu;
+        acc13 += (t >> 8) & 0x00ff00ffu;
+        s16_quad_step<G, Q + 1>(d, src, acc02, acc13);
+    }
+}
+
+// 16-bit slot build, the first 256 elements with four per lane: one ds_read2_b32 per
+// channel (the lane's two aligned dwords around its 4 bytes: 4 LDS cycles for 256
+// positions, where two ds_read_u8 per 128 positions take 8), the 4 bytes by v_alignbyte
+// (src mod 4, uniform per channel), even and odd bytes summed as u16 pairs (no carry
+// crosses: each half <= G 255).  ea / eb = the lane's (R[4l], R[4l+1]) / (R[4l+2], R[4l+3]).
+template <int G>
+__device__ __forceinline__ void s16_quad(const uint32_t (&src)[G], uint32_t smem_addr, int lane, uint32_t &ea,
+                                         uint32_t &eb)
+{
+    u32x2 d[G];
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+        const uint32_t a = smem_addr + (src[q] & ~3u) + 4u * (uint32_t)lane;
+        asm volatile("ds_read2_b32 %0, %1 offset1:1" : "=&v"(d[q]) : "v"(a) : "memory");
+    }
+    uint32_t acc02 = 0, acc13 = 0;
+    s16_quad_step<G, 0>(d, src, acc02, acc13);
+    ea = __builtin_amdgcn_perm(acc13, acc02, 0x05040100u);
+    eb = __builtin_amdgcn_perm(acc13, acc02, 0x07060302u);
+}
+
+// chunks C .. CEND - 1 of the 128-element build, issued ahead as s16_run expects
+template <int G, int P, int C, int CEND>
+__device__ __forceinline__ void s16_issue_range(uint32_t (&rb)[P][G][2], const uint32_t (&ad)[G])
+{
+    if constexpr (C < CEND) {
+        s16_issue<G, P, C>(rb, ad);
+        s16_issue_range<G, P, C + 1, CEND>(rb, ad);
     }
 }
 
@@ -481,6 +535,7 @@ __device__ __forceinline__ void s16_run(uint32_t (&rb)[P][G][2], const uint32_t 
         s16_run<G, P, C + 1, NCH>(rb, ad, e);
     }
 }
+
 
 __device__ __forceinline__ void issue_window1(u32x2 &w, uint32_t addr)
 {
@@ -832,7 +887,7 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
     // 0-2 always (len <= 512; a chunk past the copy's end stores only its lanes inside it),
     // chunk 3 when len > 384; the reads of the next 8 / G chunks in flight while a chunk is
     // summed.
-    auto slot16 = [&](const meta_t &m) {
+    auto slot16_pairs = [&](const meta_t &m) {
         const bool four = m[0] > 384;
         auto odd = [&](uint32_t e, uint32_t enext) {  // (R[2k + 1], R[2k + 2]) of lane k
             const uint32_t x = (uint32_t)__builtin_amdgcn_mov_dpp((int)enext, 0x134, 0xf, 0xf, false);  // wave_rol:1
@@ -876,6 +931,86 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
         store(c0 + 2u * cbu - 4u, e0, e1, e2, e3);
         store(c0 + cbu, o0, o1, o2, o3);
         store(c0 + 3u * cbu - 4u, o0, o1, o2, o3);
+    };
+
+    auto slot16_quad = [&](const meta_t &m) {
+        const int len = m[0];  // 256 (= TT) .. 510
+        auto odd = [&](uint32_t e, uint32_t enext) {  // (R[2k + 1], R[2k + 2]) of lane k
+            const uint32_t x = (uint32_t)__builtin_amdgcn_mov_dpp((int)enext, 0x134, 0xf, 0xf, false);  // wave_rol:1
+            const uint32_t y = (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)e, 0x130, 0xf, 0xf, false);  // wave_shl:1
+            return __builtin_amdgcn_alignbit(y, e, 16);
+        };
+        // the next lane's value (lane 63: lane 0 of `next`)
+        auto nextlane = [&](uint32_t v, uint32_t next) {
+            const uint32_t x = (uint32_t)__builtin_amdgcn_mov_dpp((int)next, 0x134, 0xf, 0xf, false);
+            return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)v, 0x130, 0xf, 0xf, false);
+        };
+        // elements 0 .. 255: four per lane (s16_quad)
+        uint32_t src[G];
+#pragma unroll
+        for (int q = 0; q < G; ++q) src[q] = (uint32_t)m[4 + q];
+        uint32_t ea, eb;
+        s16_quad<G>(src, smem_addr, lane, ea, eb);
+        // elements 256 .. len - 1 (<= 2 chunks of 128): two per lane, as chunks 2 and 3 of the
+        // 128-element build (its reads in flight per s16_run)
+        uint32_t ad[G];
+#pragma unroll
+        for (int q = 0; q < G; ++q) ad[q] = smem_addr + src[q] + 2u * (uint32_t)lane;
+        constexpr int P = 8 / G;
+        uint32_t rb[P][G][2];
+        uint32_t e[4] = {0u, 0u, 0u, 0u};
+        const bool t2 = len > 256, t3 = len > 384;
+        if (t3) {
+            s16_issue_range<G, P, 2, (2 + P < 4 ? 2 + P : 4)>(rb, ad);
+            s16_run<G, P, 2, 4>(rb, ad, e);
+        } else if (t2) {
+            s16_issue_range<G, P, 2, 3>(rb, ad);
+            s16_run<G, P, 2, 3>(rb, ad, e);
+        }
+        // dword j of copy s: copy 0 E[j], copy 1 O[j], copy 2 E[j + 1], copy 3 O[j + 1]
+        // (E[k] = (R[2k], R[2k+1]), O[k] = (R[2k+1], R[2k+2])); lane l of the first 256
+        // elements owns dwords 2l and 2l + 1: E[2l] = ea, E[2l+1] = eb
+        const uint32_t nea = nextlane(ea, e[2]);  // E[2l + 2] (lane 63: the tail's first pair)
+        const uint32_t neb = nextlane(eb, e[2]);  // E[2l + 3] (lane 63's is rewritten by the tail)
+        u32x2 w0 = {ea, eb}, w2 = {eb, nea};
+        u32x2 w1 = {__builtin_amdgcn_alignbit(eb, ea, 16), __builtin_amdgcn_alignbit(nea, eb, 16)};
+        u32x2 w3 = {w1.y, __builtin_amdgcn_alignbit(neb, nea, 16)};
+        const uint32_t c0 = lds_base + (uint32_t)m[1];
+        const uint32_t cbu = (uint32_t)copy_bytes;
+        const uint32_t a0 = c0 + 8u * (uint32_t)lane;
+        asm volatile("ds_write_b64 %0, %1" : : "v"(a0), "v"(w0) : "memory");
+        asm volatile("ds_write_b64 %0, %1" : : "v"(a0 + cbu), "v"(w1) : "memory");
+        asm volatile("ds_write_b64 %0, %1" : : "v"(a0 + 2u * cbu), "v"(w2) : "memory");
+        asm volatile("ds_write_b64 %0, %1" : : "v"(a0 + 3u * cbu), "v"(w3) : "memory");
+        if (t2) {
+            // the tail chunks by ds_write_addtid_b32 (copies 2 / 3 4 bytes down, after the
+            // first part's stores: its copy-3 dword 127 is rewritten here); a chunk reaching
+            // past its copy (copies hold TT + span + 2 elements rounded to 64) stores only its
+            // lanes inside it (elements 128 c + 2 l <= copy - 2)
+            const uint32_t o2 = odd(e[2], e[3]), o3 = odd(e[3], e[3]);
+            const bool in2 = 768u <= cbu || 512 + 4 * lane <= (int)cbu - 4;
+            const bool in3 = t3 && (1024u <= cbu || 768 + 4 * lane <= (int)cbu - 4);
+            auto store = [&](uint32_t base, uint32_t v2, uint32_t v3) {
+                asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(base) : "memory");
+                if (in2) asm volatile("ds_write_addtid_b32 %0 offset:512" : : "v"(v2) : "memory");
+                if (in3) asm volatile("ds_write_addtid_b32 %0 offset:768" : : "v"(v3) : "memory");
+            };
+            store(c0, e[2], e[3]);
+            store(c0 + 2u * cbu - 4u, e[2], e[3]);
+            store(c0 + cbu, o2, o3);
+            store(c0 + 3u * cbu - 4u, o2, o3);
+        }
+    };
+
+    // G = 8: the first 256 elements four per lane (s16_quad: half the build's LDS read cycles;
+    // round 6 A/B: C3 625 trials 115.5 -> 113.5 ms, 5000 958 -> 936 ms); G <= 4: two per lane
+    // throughout, which measured faster there (5000 trials G = 4: 858 vs 901 ms) - with 2 G
+    // byte reads per chunk, 8 / G chunks stay in flight
+    auto slot16 = [&](const meta_t &m) {
+        if constexpr (G == 8)
+            slot16_quad(m);
+        else
+            slot16_pairs(m);
     };
 
     // ---- build the stage's slots, one per wave at a time: R[i] (i < len) at copy 0 [i]
@@ -1757,11 +1892,11 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     const int64_t eb = dma8 ? 1 : 4;  // bytes per staged raw element
     // 16-bit integer slots: 8-bit DMA rows in 256-sample time tiles; four
     // alignment copies of >= 384 u16 elements, slots of <= 512 elements (span <= kS16Span)
-    // G <= 4 only: G = 8 with 16-bit slots measured slower than with float32 slots (C3 625
-    // trials 140.6 vs 115.1 ms, 5000: 1055 vs 960; G = 4: 126.6 / 909.7 ms - DESIGN.md §4.1b,
-    // profiles/r06/experiments/slot16/)
-    const int s16opt = pu::knob("PU_SLOT16", p->opt_slot16);  // -1 auto (G <= 4), 0 off, 1 any G
-    const bool s16 = dma8 && TT == 256 && (s16opt > 0 || (s16opt < 0 && G <= 4));
+    // Every G: with the four-per-lane build G = 8 is faster with 16-bit slots too (C3 625
+    // trials 113.5 vs 114.3 ms, 5000: 936 vs 957 - DESIGN.md §4.1b, profiles/r06/experiments/
+    // slot16/); the per-window cost term below makes the planner pick G per grid
+    const int s16opt = pu::knob("PU_SLOT16", p->opt_slot16);  // -1 auto (= on), 0 off, 1 on
+    const bool s16 = dma8 && TT == 256 && s16opt != 0;
     const int64_t ncopies = s16 ? 4 : 2;
     const bool pack_cover = n < (int64_t(1) << 24);  // row bases fit 24 bits: covers above them
     // a stage's raw rows (DMA mode) and its slots share the LDS budget; a stage holds

@@ -706,26 +706,25 @@ def test_slot16_u8_wrapping_windows_and_small_budget(gpu, budget):
     _tables_agree(r16, r32)
 
 
-def test_slot16_declined_for_group_8(gpu):
-    """By default the planner keeps float32 slots for G = 8 (16-bit slots measured slower
-    there: DESIGN.md §4.1b) and uses 16-bit slots for G <= 4; slot16=True forces them for
-    any group size, slot16=False never."""
+def test_slot16_default_every_group(gpu):
+    """By default the planner uses 16-bit slots for 8-bit rows in 256-sample tiles at every
+    group size (G = 8 with the four-per-lane build measured faster than with float32 slots:
+    DESIGN.md §4.1b); slot16=True is the same, slot16=False never uses them."""
     x = np.zeros((64, 4096), np.uint8)
     sh = _hip.shift_table(64, np.linspace(0, 50, 40), 400., 100., 1e-3)
     mk = lambda g, s16: _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, 64, 4096, sh, group=g, shape="tall",
                                    slot16=s16).info
-    assert mk(8, None)["kernel"] == 2 and mk(4, None)["kernel"] == 3 and mk(2, None)["kernel"] == 3
-    assert mk(8, True)["kernel"] == 3 and mk(4, False)["kernel"] == 2
+    assert mk(8, None)["kernel"] == 3 and mk(4, None)["kernel"] == 3 and mk(2, None)["kernel"] == 3
+    assert mk(8, True)["kernel"] == 3 and mk(4, False)["kernel"] == 2 and mk(8, False)["kernel"] == 2
 
 
 def test_c3_plan_choice_shard_and_full(gpu):
     """The planner's cost model at C3's two measured operating points:
-    the 625-trial shard of the 8-GPU split keeps tall G = 8 with float32 slots (114.2 vs
-    121.3 ms for 16-bit G = 4), the whole 5000-trial grid takes tall G = 4 with 16-bit slots
-    (858 vs 954 ms)."""
+    the 625-trial shard of the 8-GPU split takes tall G = 8 (16-bit slots 113.5 ms, against
+    127.2 ms for G = 4), the whole 5000-trial grid tall G = 4 (858 ms, against 936 for G = 8)."""
     c = CONFIGS["C3"]
     dms = D.dedispersion_plan(c.nchan, c.dmmin, c.dmmax, c.start_freq, c.bandwidth, c.tsamp)
-    for ntr, group, kernel in ((625, 8, 2), (5000, 4, 3)):
+    for ntr, group, kernel in ((625, 8, 3), (5000, 4, 3)):
         sh = _hip.shift_table(c.nchan, dms[:ntr], c.start_freq, c.bandwidth, c.tsamp)
         info = _hip.Plan(_hip.PU_U8, _hip.PU_ACC_NATIVE, c.nchan, c.nsamples, sh).info
         assert (info["group"], info["kernel"], info["trials_per_tile"]) == (group, kernel, 256), (ntr, info)
