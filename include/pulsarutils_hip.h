@@ -88,8 +88,8 @@ typedef struct pu_plan_opts {
     int32_t u8_dma;         /* -1 auto (8-bit rows by LDS-DMA when n % 4 == 0), 0 global-memory build */
     int32_t dt_major;       /* -1 auto item order, 0 time-tile major, 1 DM-tile major */
     int32_t slot16;         /* 16-bit integer slots for 8-bit rows by LDS-DMA in 256-sample
-                             * time tiles: -1 auto (groups of <= 4 channels), 0 never
-                             * (float32 slots), 1 any group size */
+                             * time tiles: -1 auto (= 1), 0 never (float32 slots), 1 every
+                             * group size (round 6: -1 meant groups of <= 4 channels) */
     int32_t reserved[2];    /* zero */
 } pu_plan_opts;
 int pu_plan_create_ex(pu_plan **plan, int dtype, int acc, int64_t nchan, int64_t nsamples,

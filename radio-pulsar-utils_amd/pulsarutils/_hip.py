@@ -241,8 +241,8 @@ class Plan:
         ``lds_budget_kb``: LDS per workgroup (0 = default); ``u8_dma``: False builds 8-bit
         slots from global memory instead of LDS-DMA'd rows; ``dt_major``: work-item order
         (None = automatic); ``slot16``: 16-bit integer slots for 8-bit DMA rows in 256-sample
-        tiles - None: for groups of <= 4 channels, False: never, True: for
-        any group size.  These are the planner's only inputs (pu_plan_create_ex): the
+        tiles - None / True: at every group size, False: never (float32
+        slots).  These are the planner's only inputs (pu_plan_create_ex): the
         library reads no environment."""
         require_gpu()
         sh = np.ascontiguousarray(shifts, dtype=np.int64)
