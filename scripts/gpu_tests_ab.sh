@@ -1,6 +1,7 @@
 #!/bin/bash
 # One GPU call: a pytest selection (PYTEST_K, -k expression; PYTEST_FILES), then interleaved
-# plan A/B sweeps (SWEEPS="cfg:trials:variants;..." -> scripts/sweep.py), each step under its
+# plan A/B sweeps (SWEEPS="cfg:trials[+first]:variants;..." -> scripts/sweep.py; "625+1875" =
+# trials 1875 .. 2499), each step under its
 # own time limit; stops at the first failure.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -16,6 +17,8 @@ for sw in "${SW[@]}"; do
   [ -z "$sw" ] && continue
   IFS=':' read -r cfg trials variants <<< "$sw"
   i=$((i+1))
-  PU_SWEEP="$variants" PU_TRIALS="$trials" PU_ROUNDS=${ROUNDS:-3} timeout -k 10 400 python -u scripts/sweep.py $cfg > $OUT/sweep_${i}_${cfg}.log 2>&1 || exit $?
+  t0=0
+  case "$trials" in *+*) t0=${trials#*+}; trials=${trials%%+*};; esac
+  PU_SWEEP="$variants" PU_TRIALS="$trials" PU_TRIAL0="$t0" PU_ROUNDS=${ROUNDS:-3} timeout -k 10 400 python -u scripts/sweep.py $cfg > $OUT/sweep_${i}_${cfg}.log 2>&1 || exit $?
 done
 echo done > $OUT/status.txt

@@ -4,7 +4,8 @@ Usage: python scripts/sweep.py [config]
   env PU_SWEEP="G:KB[:shape],..." selects (channel-group size, LDS budget KB, subband
   workgroup shape 0 wide / 1 pair / 2 tall[, slot16 0/1]) variants, e.g.
   "1:64,4:160:0,4:80:1" (group 1 = channel mode), "8:160:2:1,8:160:2:0" (8-bit C3: 16-bit vs
-  float32 slots).  PU_ROUNDS rounds, PU_TRIALS the first trials of the grid.
+  float32 slots).  PU_ROUNDS rounds, PU_TRIALS the first trials of the grid (from trial
+  PU_TRIAL0, default 0: e.g. PU_TRIAL0=1875 PU_TRIALS=625 is rank 3's shard of 8 at C3).
 Prints one line per (variant, round) and a median summary; the S/N of every trial
 is compared with the first variant's (float32 tolerance).
 """
@@ -25,8 +26,9 @@ rounds = int(os.environ.get("PU_ROUNDS", "3"))
 ntrials = int(os.environ.get("PU_TRIALS", "0"))
 x = synth.pulsar_filterbank_device(cfg)
 dms = dedispersion_plan(cfg.nchan, cfg.dmmin, cfg.dmmax, cfg.start_freq, cfg.bandwidth, cfg.tsamp)
-if ntrials:
-    dms = dms[:ntrials]
+trial0 = int(os.environ.get("PU_TRIAL0", "0"))
+if ntrials or trial0:
+    dms = dms[trial0:trial0 + ntrials] if ntrials else dms[trial0:]
 sh = _hip.shift_table(cfg.nchan, dms, cfg.start_freq, cfg.bandwidth, cfg.tsamp)
 plans = {}
 for v in variants:
