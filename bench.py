@@ -8,12 +8,17 @@ Scaling (one process per GPU, torchrun; DM trials are independent: the one excha
 the data path is the filterbank's distribution from rank 0 - DESIGN.md §5):
 * N = 1 (default): C2, 1000 trials, the filterbank resident in HBM.
 * N > 1 (default): BASELINE.json configs[2] as stated - C3 (4096 chan x 2^22 uint8,
-  17.2 GB) held by rank 0, its 5000 trials split contiguously over the N ranks
-  (``--scaling strong``; C3 at N = 8: 625 trials per GPU).  One timed step is the whole
-  job: the filterbank distributed from rank 0 in time chunks (``--collective``,
-  default scatter + all-gather over the xGMI mesh) with each rank's search of the time
-  tiles whose rows have landed overlapping the later chunks, the finalize, and the
-  all_gather of the per-trial (max, std, snr, rebin).  ``value`` = 5000 x 2^22 / step.
+  17.2 GB) held by rank 0, its 5000 trials searched by the N ranks together
+  (``--scaling strong``).  ``--decomposition time`` (default, round 6): every rank searches
+  its 1/N of the time tiles for all 5000 trials (the whole grid's 20 DM tiles, where N DM
+  slices would add DM tiles whose fixed cost does not shrink with their trial count,
+  DESIGN.md §5), the per-(trial, tile) records go to the trial owners (one all_to_all) and
+  each rank finalizes its 5000 / N trials; ``dm``: each rank searches its contiguous DM
+  slice (625 trials at N = 8).  One timed step is the whole job: the filterbank
+  distributed from rank 0 in time chunks (``--collective``, default scatter + all-gather
+  over the xGMI mesh) with each rank's search of its tiles whose rows have landed
+  overlapping the later chunks, the finalize, and the all_gather of the per-trial
+  (max, std, snr, rebin).  ``value`` = 5000 x 2^22 / step.
 * ``--scaling weak``: the DM grid is N x ``ntrials`` trials of ``--config`` (C2), rank r
   owns trials [r ntrials, (r+1) ntrials); the filterbank is distributed before timing.
 ``multi_gpu`` (N > 1) reports the whole-filterbank exchange alone and one pipelined
@@ -43,7 +48,7 @@ import torch.distributed as dist  # noqa: E402
 from pulsarutils import _hip, synth  # noqa: E402
 from pulsarutils.configs import CONFIGS  # noqa: E402
 from pulsarutils.dedispersion import dedispersion_plan  # noqa: E402
-from pulsarutils.parallel import pipelined_broadcast_search, shard_bounds  # noqa: E402
+from pulsarutils.parallel import pipelined_broadcast_search, shard_bounds, tile_sharded_search  # noqa: E402
 
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
 HBM_PEAK_GBS = 8000.0
@@ -321,7 +326,7 @@ def c3_strong(dev, world, rank, steps, chunks):
     return res
 
 
-def exchange_bench(x, plan, outs, ws, dev, chunks):
+def exchange_bench(x, plan, outs, ws, dev, chunks, decomposition="dm"):
     """N > 1: the whole filterbank distributed from rank 0 by each collective alone
     (``*_ms``, ``*_GBps`` = bytes / time), then one pipelined step per collective (chunked
     exchange + the search of each time tile as soon as its rows and halo landed +
@@ -343,16 +348,29 @@ def exchange_bench(x, plan, outs, ws, dev, chunks):
     res = {"bytes": nbytes, "bcast_chunks": chunks, "end_to_end_ms": {},
            "what": "<collective>_ms: the whole filterbank from rank 0 by that exchange alone; end_to_end_ms: one "
                    "chunked exchange pipelined with the search (each time tile launched once its rows and halo "
-                   "landed) and the finalize"}
+                   "landed) and the finalize - per collective with the whole filterbank to every rank, and "
+                   "(time split) 'sliced': each rank receives only the columns its time tiles read"}
     for c in COLLECTIVES:
         timed(lambda: broadcast_filterbank(x, src=0, collective=c))  # warm-up (communicator setup)
         ms = timed(lambda: broadcast_filterbank(x, src=0, collective=c))
         res[f"{c}_ms"] = ms
         res[f"{c}_GBps"] = round(nbytes / ms / 1e6, 1)
     for c in COLLECTIVES:
-        res["end_to_end_ms"][c] = timed(lambda: pipelined_broadcast_search(x, plan, outs, ws, src=0, chunks=chunks,
-                                                                          collective=c))
-    res["search_only_ms"] = timed(lambda: plan.search(x, out=outs, workspace=ws))
+        if decomposition == "time":
+            fn = (lambda: tile_sharded_search(x, plan, outs, ws, src=0, chunks=chunks, collective=c, full_copy=True))
+        else:
+            fn = (lambda: pipelined_broadcast_search(x, plan, outs, ws, src=0, chunks=chunks, collective=c))
+        res["end_to_end_ms"][c] = timed(fn)
+    if decomposition == "time":
+        # the default time split: each rank receives only the columns its tiles read
+        res["end_to_end_ms"]["sliced"] = timed(lambda: tile_sharded_search(x, plan, outs, ws, src=0, chunks=chunks))
+    if decomposition == "time":
+        t0, t1 = shard_bounds(plan.info["time_tiles"], dist.get_world_size(), dist.get_rank())
+        res["search_only_ms"] = timed(lambda: plan.search_tiles(x, t0, t1, ws))
+        res["search_only_what"] = "each rank's time tiles of the whole grid (pu_plan_search_tiles), resident data"
+    else:
+        res["search_only_ms"] = timed(lambda: plan.search(x, out=outs, workspace=ws))
+    res["decomposition"] = decomposition
     return res
 
 
@@ -367,6 +385,13 @@ def main():
                     help="default: weak (one GPU: the single-GPU workload), strong on N > 1")
     ap.add_argument("--collective", default="scatter_allgather", choices=["broadcast", "scatter_allgather"],
                     help="N > 1: the chunk exchange inside the timed strong-scaling step")
+    ap.add_argument("--decomposition", default="time", choices=["time", "dm"],
+                    help="N > 1 strong split: time - every rank searches its slice of the time tiles for the "
+                         "whole grid, the per-tile records go to the trial owners (parallel.tile_sharded_search); "
+                         "dm - every rank plans and searches its contiguous DM slice")
+    ap.add_argument("--full-copy", action="store_true",
+                    help="time split: send the whole filterbank to every rank (--collective) instead of scattering "
+                         "to each rank the columns its time tiles read")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the N > 1 path with every rank on the visible GPU(s), round robin "
                          "(RCCL refuses two ranks on one device); timings are then not the product's")
@@ -435,6 +460,8 @@ def main():
     dms = dms_all[lo:hi]
     per_rank = dms.size
     chunk = -(-dms_all.size // world)  # equal gather slots
+    pipelined = world > 1 and args.scaling == "strong"
+    tsplit = pipelined and args.decomposition == "time"
 
     # ---- input: generated on rank 0 in HBM, RCCL-broadcast to the others
     t0 = time.perf_counter()
@@ -447,26 +474,35 @@ def main():
     log(f"rank {rank}: input ready {time.perf_counter() - t0:.1f}s")
 
     acc = {"native": _hip.PU_ACC_NATIVE, "f32": _hip.PU_ACC_F32, "f64": _hip.PU_ACC_F64}[args.acc]
-    sh = _hip.shift_table(cfg.nchan, dms, cfg.start_freq, cfg.bandwidth, cfg.tsamp)
+    # time split: every rank plans the whole grid (and searches its slice of the time tiles)
+    sh = _hip.shift_table(cfg.nchan, dms_all if tsplit else dms, cfg.start_freq, cfg.bandwidth, cfg.tsamp)
     plan = _hip.Plan(_hip.dtype_code(x.dtype), acc, cfg.nchan, cfg.nsamples, sh)
     log(f"rank {rank}: plan {plan.info}")
     ws = torch.empty(plan.workspace_bytes, dtype=torch.uint8, device=dev)
-    outs = (torch.empty(per_rank, dtype=torch.float64, device=dev),
-            torch.empty(per_rank, dtype=torch.float64, device=dev),
-            torch.empty(per_rank, dtype=torch.float64, device=dev),
-            torch.empty(per_rank, dtype=torch.int32, device=dev))
+    nout = plan.ndm
+    outs = (torch.empty(nout, dtype=torch.float64, device=dev),
+            torch.empty(nout, dtype=torch.float64, device=dev),
+            torch.empty(nout, dtype=torch.float64, device=dev),
+            torch.empty(nout, dtype=torch.int32, device=dev))
+    o_lo, o_hi = (lo, hi) if tsplit else (0, per_rank)  # this rank's trials in outs
+    tt0, tt1 = (shard_bounds(plan.info["time_tiles"], world, rank) if tsplit else (0, plan.info["time_tiles"]))
     local_stats = torch.zeros((4, chunk), dtype=torch.float64, device=dev)
     gathered = torch.empty((world * 4, chunk), dtype=torch.float64, device=dev)  # rank-major (4, chunk) blocks
 
     bcast = None
-    pipelined = world > 1 and args.scaling == "strong"
     if world > 1:
-        bcast = exchange_bench(x, plan, outs, ws, dev, args.bcast_chunks)
+        bcast = exchange_bench(x, plan, outs, ws, dev, args.bcast_chunks, args.decomposition if pipelined else "dm")
         if rank == 0:
             log(f"exchange {bcast}")
 
     def step(phases=None):
-        if pipelined:
+        if tsplit:
+            # the whole job: rank 0's filterbank distributed in interleaved time chunks, every
+            # rank searching its time tiles of the whole grid as they land, the records to the
+            # trial owners, each owner's finalize
+            tile_sharded_search(x, plan, outs, ws, src=0, chunks=args.bcast_chunks, collective=args.collective,
+                                phases=phases, full_copy=args.full_copy)
+        elif pipelined:
             # the whole job: rank 0's filterbank distributed in time chunks, every rank
             # searching the tiles whose rows have landed, then the finalize
             pipelined_broadcast_search(x, plan, outs, ws, src=0, chunks=args.bcast_chunks,
@@ -476,7 +512,8 @@ def main():
         if world > 1:
             if phases is not None:
                 phases.mark("gather", torch.cuda.current_stream(dev))
-            local_stats[:, :per_rank].copy_(torch.stack([outs[0], outs[1], outs[2], outs[3].to(torch.float64)]))
+            local_stats[:, :per_rank].copy_(torch.stack([outs[0][o_lo:o_hi], outs[1][o_lo:o_hi], outs[2][o_lo:o_hi],
+                                                         outs[3][o_lo:o_hi].to(torch.float64)]))
             dist.all_gather_into_tensor(gathered, local_stats)
             if phases is not None:
                 phases.mark("gather", torch.cuda.current_stream(dev), end=True)
@@ -523,7 +560,8 @@ def main():
         allv = allv.view(world, len(keys)).cpu().numpy()
         phase_ms = {"what": "one extra untimed step with HIP events: per-chunk exchange (scatter + all-gather "
                             "or broadcast) and unpack (staging -> strided column chunk, receivers) on the "
-                            "communication stream, tile searches per chunk, finalize, gather; exposed_tail = "
+                            "communication stream, tile searches per chunk, records all_to_all (time split), "
+                            "finalize, gather; exposed_tail = "
                             "last chunk landed -> finalize done",
                     "rank0": mine, "max_over_ranks": {k: round(float(allv[:, i].max()), 4) for i, k in enumerate(keys)}}
 
@@ -540,7 +578,9 @@ def main():
     value = total_samples / (ms_per_step / 1e3)
     # kernel time per step (pipelined: the sum of the step's tile-range launches)
     kernel_ms = float(np.sum(kms)) / args.steps if len(kms) else None
-    adds = float(cfg.nchan) * cfg.nsamples * per_rank
+    # per rank: its trials x every sample, or (time split) every trial x its time tiles
+    adds = (float(cfg.nchan) * min(cfg.nsamples, tt1 * plan.info["time_tile"]) - float(cfg.nchan) * tt0
+            * plan.info["time_tile"]) * plan.ndm
     esz = {"f32": 4, "u8": 1, "f64": 8}[cfg.dtype]
     alg_bytes = float(cfg.nchan) * cfg.nsamples * esz  # compulsory input read per launch (stats mode)
     roof = None
@@ -550,6 +590,8 @@ def main():
         peak = VALU_F64_ADD_PEAK_TFLOPS if acc64 else VALU_ADD_PEAK_TFLOPS
         achieved = adds / (kernel_ms / 1e3) / 1e12
         pmc_tag = args.config if per_rank == cfg.ntrials else f"{args.config}_{per_rank}"
+        if tsplit:
+            pmc_tag = f"{args.config}_time{world}"  # no committed counters for a rank's time slice
         pmc, pmc_same = load_pmc(pmc_tag)
         # counter traffic only when it was collected from this kernel source
         traffic = pmc.get("hbm_bytes_per_launch") if pmc and pmc_same else None
@@ -655,9 +697,17 @@ def main():
                                       f"{cfg.dtype} samples, {dms_all.size} DM trials "
                                       f"({'per GPU' if args.scaling == 'weak' else 'in all'})",
                            "nchan": cfg.nchan, "nsamples": cfg.nsamples, "trials_per_gpu": per_rank,
-                           "total_trials": int(dms_all.size), "parallelism": f"dm-shard{world}",
+                           "total_trials": int(dms_all.size),
+                           "parallelism": f"time-shard{world}" if tsplit else f"dm-shard{world}",
                            "best_dm": best_dm},
-                "step": ("chunked filterbank exchange from rank 0 (%s) pipelined with each rank's search of its "
+                "step": ("%s pipelined with each rank's search of its time tiles for every trial, all_to_all of "
+                         "the per-tile records to the trial owners, finalize of each rank's trials, all_gather of "
+                         "(max, std, snr, rebin)" % ("interleaved chunked filterbank exchange from rank 0 (%s)"
+                                                     % args.collective if args.full_copy else
+                                                     "chunked scatter from rank 0 of the columns each rank's time "
+                                                     "tiles read")
+                         if tsplit else
+                         "chunked filterbank exchange from rank 0 (%s) pipelined with each rank's search of its "
                          "DM slice, finalize, all_gather of (max, std, snr, rebin)" % args.collective
                          if pipelined else "pu_plan_search of the resident filterbank" +
                          (" + all_gather of (max, std, snr, rebin)" if world > 1 else "")),

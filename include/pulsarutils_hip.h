@@ -119,6 +119,45 @@ int pu_plan_finalize(pu_plan *plan, const void *data, int64_t ld, double *max_ou
                      double *std_out, double *snr_out, int32_t *rebin_out, void *workspace,
                      size_t workspace_bytes, void *stream);
 
+/* pu_plan_finalize of trials [trial_begin, trial_end) only (time-tile sharding across
+ * GPUs, DESIGN.md §5: each rank searches a range of time tiles for every trial, the
+ * per-tile records of each trial are moved to the rank that owns the trial, and the owner
+ * finalizes its trials).  The records are the workspace's first bytes, trial-major:
+ * record (trial d, time tile t) = rec_stride elements of rec_elem_bytes (float32 or
+ * float64) at element (d ntt + t) rec_stride (pu_plan_info "rec_elem_bytes",
+ * "rec_stride"); only the range's records are read.  Outputs are indexed by plan trial
+ * (arrays of ndm; only [trial_begin, trial_end) written).  Certification as in
+ * pu_plan_finalize (flagged trials recomputed exactly from data, which must then hold the
+ * whole filterbank).  The replaced reference code is the same (dedispersion.py:174-202). */
+int pu_plan_finalize_range(pu_plan *plan, const void *data, int64_t ld, int64_t trial_begin,
+                           int64_t trial_end, double *max_out, double *std_out, double *snr_out,
+                           int32_t *rebin_out, void *workspace, size_t workspace_bytes, void *stream);
+
+/* The finalize of trials [trial_begin, trial_end) without the exact recomputation, for
+ * time-tile sharding where each rank holds only its time slice of the filterbank
+ * (DESIGN.md §5): the fast statistics are written (outputs indexed by plan trial) and the
+ * trials certification would recompute are returned instead - counts[0] = how many,
+ * counts[1] = of which with a non-finite partial; the first min(count, cap) plan trial
+ * indices into flagged (host, ascending).  Synchronises stream.  The caller settles them
+ * (pulsarutils.parallel: a non-finite input anywhere -> the NaN rule for every trial;
+ * otherwise each rank's slice of pu_plan_exact_series, gathered, + pu_series_stats). */
+int pu_plan_finalize_range_flagged(pu_plan *plan, int64_t trial_begin, int64_t trial_end,
+                                   double *max_out, double *std_out, double *snr_out, int32_t *rebin_out,
+                                   void *workspace, size_t workspace_bytes, int32_t *flagged, int64_t cap,
+                                   int64_t *counts, void *stream);
+
+/* The reference's float64 dedispersed series (channel order, dedispersion.py:86-98, bit
+ * for bit) of m plan trials (host indices) into out (device, m x nsamples contiguous).
+ * Sample t reads column (t + shift) mod nsamples of each channel: with only part of the
+ * filterbank present, the samples whose columns are present are exact.  Synchronises. */
+int pu_plan_exact_series(pu_plan *plan, const void *data, int64_t ld, const int32_t *trials, int64_t m,
+                         double *out, void *stream);
+
+/* *flag (device int32) = 1 if any of the nrows x ncols float32 / float64 elements (row
+ * stride ld) is NaN or +-inf, else 0 (always 0 for uint8).  Asynchronous on stream. */
+int pu_nonfinite_any(const void *data, int dtype, int64_t nrows, int64_t ncols, int64_t ld, int32_t *flag,
+                     void *stream);
+
 /* Certification (pu_plan_search and pu_plan_finalize).  The fast
  * path's per-trial statistics are summed in another order than numpy's; a trial whose
  * result that order could change - a zero or rounding-level std (constant input), a
@@ -178,14 +217,15 @@ int pu_plan_stamps(pu_plan *plan, int64_t *out, int n);
  * {ndm, dm_tiles, time_tiles, trials_per_tile, time_tile, chans_per_step,
  *  row_stride, lds_bytes, acc_is_f64, max_spread, group, slots, stages,
  *  slot_bytes, raw_stride, exec_adds, lds_traffic, cert_rechecked, cert_nan, cert_std,
- *  cert_sign, cert_tie, cert_us, kernel}: exec_adds and lds_traffic are the adds and LDS bytes (reads,
+ *  cert_sign, cert_tie, cert_us, kernel, rec_elem_bytes, rec_stride}: exec_adds and lds_traffic are the adds and LDS bytes (reads,
  *  writes, DMA) one launch executes (subband mode; 0 otherwise); the cert_* fields
  *  describe the last search's certification step (see pu_plan_finalize): trials
  *  recomputed, the NaN rule, and how many trials each check flagged (std not above its
  *  rounding bound, S/N sign, S/N tie) and the host microseconds spent settling them;
  *  kernel: 0 dedisp_kernel (channel order), 1 dedisp_f64_kernel, 2 dedisp_sub_kernel
- *  (float32 slots), 3 dedisp_sub_kernel with 16-bit integer slots (8-bit input).
- *  Returns the count written. */
+ *  (float32 slots), 3 dedisp_sub_kernel with 16-bit integer slots (8-bit input);
+ *  rec_elem_bytes / rec_stride: the per-(trial, time tile) record layout at the start of
+ *  the workspace (pu_plan_finalize_range).  Returns the count written. */
 int pu_plan_info(const pu_plan *plan, int64_t *info, int n);
 
 /* ------------------------------------------------------------------ streams */

@@ -1226,10 +1226,10 @@ template <typename PT>
 __global__ void __launch_bounds__(256)
 pu_finalize_kernel(const PT *__restrict__ part, int ntt, int n, int tt_len,
                    double *max_out, double *std_out, double *snr_out, int32_t *win_out,
-                   CertModel cm, CertState *cert, int32_t *list)
+                   CertModel cm, CertState *cert, int32_t *list, int first)
 {
     __shared__ double red[4][4][256];
-    const int trial = blockIdx.x;
+    const int trial = first + (int)blockIdx.x;  // trials [first, first + gridDim.x) of the plan
     const int tid = threadIdx.x;
     const PT *p = part + (size_t)trial * ntt * kPartStride;
     const double mu = p[0];
@@ -2339,21 +2339,24 @@ CertModel cert_model(const pu_plan *p)
     return m;
 }
 
-// cleared: the caller already zeroed the certification state earlier in the stream
+// cleared: the caller already zeroed the certification state earlier in the stream.
+// Trials [first, first + count) (count < 0: every trial); outputs indexed by plan trial.
 int launch_finalize(pu_plan *p, const void *part, double *mx, double *sd, double *snr, int32_t *win, char *ws,
-                    hipStream_t s, bool cleared = false)
+                    hipStream_t s, bool cleared = false, int64_t first = 0, int64_t count = -1)
 {
     CertState *cert = reinterpret_cast<CertState *>(ws + part_bytes(p));
     int32_t *list = reinterpret_cast<int32_t *>(cert + 1);
     if (!cleared) PU_TRY_HIP(hipMemsetAsync(cert, 0, sizeof(CertState), s));
+    if (count < 0) count = p->ndm - first;
+    if (count == 0) return PU_OK;
     if (part_elem(p) == sizeof(float))
-        hipLaunchKernelGGL(pu_finalize_kernel<float>, dim3((unsigned)p->ndm), dim3(256), 0, s,
+        hipLaunchKernelGGL(pu_finalize_kernel<float>, dim3((unsigned)count), dim3(256), 0, s,
                            reinterpret_cast<const float *>(part), p->ntt, (int)p->n, p->TT, mx, sd, snr, win, cert_model(p),
-                           cert, list);
+                           cert, list, (int)first);
     else
-        hipLaunchKernelGGL(pu_finalize_kernel<double>, dim3((unsigned)p->ndm), dim3(256), 0, s,
+        hipLaunchKernelGGL(pu_finalize_kernel<double>, dim3((unsigned)count), dim3(256), 0, s,
                            reinterpret_cast<const double *>(part), p->ntt, (int)p->n, p->TT, mx, sd, snr, win, cert_model(p),
-                           cert, list);
+                           cert, list, (int)first);
     return pu::launch_check("pu_finalize_kernel");
 }
 
@@ -2365,8 +2368,9 @@ int launch_finalize(pu_plan *p, const void *part, double *mx, double *sd, double
 // few trials a search flags) + pu_series_stats - in batches that fit ~1 GiB of
 // stream-ordered scratch allocated for the call.
 int resolve_flagged(pu_plan *p, const void *data, int64_t ld, double *mx, double *sd, double *snr, int32_t *win,
-                    char *ws, hipStream_t s)
+                    char *ws, hipStream_t s, int64_t first = 0, int64_t count = -1)
 {
+    if (count < 0) count = p->ndm - first;
     CertState *cert = reinterpret_cast<CertState *>(ws + part_bytes(p));
     const int32_t *list = reinterpret_cast<const int32_t *>(cert + 1);
     p->cert_rechecked = 0;
@@ -2397,7 +2401,7 @@ int resolve_flagged(pu_plan *p, const void *data, int64_t ld, double *mx, double
             // so a NaN / inf anywhere reaches every trial: np.mean -> NaN or inf, the
             // shifted series -> NaN, max = std = NaN, no S/N beats 0 (dedispersion.py:186-201)
             p->cert_nan = 1;
-            int rc2 = pu::nan_rule(p->ndm, mx, sd, snr, win, s);
+            int rc2 = pu::nan_rule(count, mx + first, sd + first, snr + first, win + first, s);
             if (rc2) return rc2;
             PU_TRY_HIP(hipStreamSynchronize(s));
             return PU_OK;
@@ -2698,7 +2702,8 @@ int pu_plan_info(const pu_plan *p, int64_t *info, int n)
                          p->row_stride, (int64_t)p->lds_bytes, kVariants[p->variant].acc_f64, p->max_spread,
                          p->group, p->nslots_total, p->nstages, (int64_t)p->slot_bytes, p->raw_stride,
                          p->exec_adds, p->lds_traffic, p->cert_rechecked, p->cert_nan, p->cert_why[0],
-                         p->cert_why[1], p->cert_why[2], p->cert_us, plan_kernel(p)};
+                         p->cert_why[1], p->cert_why[2], p->cert_us, plan_kernel(p), (int64_t)part_elem(p),
+                         kPartStride};
     const int m = std::min<int>(n, (int)(sizeof v / sizeof v[0]));
     for (int k = 0; k < m; ++k) info[k] = v[k];
     return m;
@@ -2763,6 +2768,105 @@ int pu_plan_finalize(pu_plan *p, const void *data, int64_t ld, double *max_out, 
     rc = launch_finalize(p, ws, max_out, std_out, snr_out, rebin_out, ws, s);
     if (rc) return rc;
     return resolve_flagged(p, data, ld, max_out, std_out, snr_out, rebin_out, ws, s);
+}
+
+int pu_plan_finalize_range(pu_plan *p, const void *data, int64_t ld, int64_t trial_begin, int64_t trial_end,
+                           double *max_out, double *std_out, double *snr_out, int32_t *rebin_out, void *workspace,
+                           size_t ws_bytes, void *stream)
+{
+    int rc = check_data(p, data, ld);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> guard(p->lock.m);
+    PU_REQUIRE(0 <= trial_begin && trial_begin <= trial_end && trial_end <= p->ndm,
+               "pu_plan_finalize_range: trial range [%lld, %lld) outside [0, %lld)", (long long)trial_begin,
+               (long long)trial_end, (long long)p->ndm);
+    PU_REQUIRE(max_out && std_out && snr_out && rebin_out, "pu_plan_finalize_range: NULL output");
+    PU_REQUIRE(workspace && ws_bytes >= pu_plan_workspace_bytes(p) && reinterpret_cast<uintptr_t>(workspace) % 8 == 0,
+               "pu_plan_finalize_range: workspace too small or not 8-byte aligned");
+    hipStream_t s = pu::as_stream(stream);
+    char *ws = reinterpret_cast<char *>(workspace);
+    rc = launch_finalize(p, ws, max_out, std_out, snr_out, rebin_out, ws, s, false, trial_begin,
+                         trial_end - trial_begin);
+    if (rc) return rc;
+    return resolve_flagged(p, data, ld, max_out, std_out, snr_out, rebin_out, ws, s, trial_begin,
+                           trial_end - trial_begin);
+}
+
+int pu_plan_finalize_range_flagged(pu_plan *p, int64_t trial_begin, int64_t trial_end, double *max_out,
+                                   double *std_out, double *snr_out, int32_t *rebin_out, void *workspace,
+                                   size_t ws_bytes, int32_t *flagged, int64_t cap, int64_t *counts, void *stream)
+{
+    PU_REQUIRE(p != nullptr, "plan is NULL");
+    std::lock_guard<std::mutex> guard(p->lock.m);
+    PU_REQUIRE(0 <= trial_begin && trial_begin <= trial_end && trial_end <= p->ndm,
+               "pu_plan_finalize_range_flagged: trial range [%lld, %lld) outside [0, %lld)", (long long)trial_begin,
+               (long long)trial_end, (long long)p->ndm);
+    PU_REQUIRE(max_out && std_out && snr_out && rebin_out && counts && (flagged || cap == 0),
+               "pu_plan_finalize_range_flagged: NULL output");
+    PU_REQUIRE(workspace && ws_bytes >= pu_plan_workspace_bytes(p) && reinterpret_cast<uintptr_t>(workspace) % 8 == 0,
+               "pu_plan_finalize_range_flagged: workspace too small or not 8-byte aligned");
+    hipStream_t s = pu::as_stream(stream);
+    char *ws = reinterpret_cast<char *>(workspace);
+    int rc = launch_finalize(p, ws, max_out, std_out, snr_out, rebin_out, ws, s, false, trial_begin,
+                             trial_end - trial_begin);
+    if (rc) return rc;
+    CertState *cert = reinterpret_cast<CertState *>(ws + part_bytes(p));
+    const int32_t *list = reinterpret_cast<const int32_t *>(cert + 1);
+    PU_TRY_HIP(hipMemcpyAsync(p->h_cert, cert, sizeof(CertState), hipMemcpyDeviceToHost, s));
+    PU_TRY_HIP(hipStreamSynchronize(s));
+    const int64_t nflag = p->h_cert->nflag;
+    counts[0] = nflag;
+    counts[1] = p->h_cert->nnonfinite;
+    for (int k = 0; k < 3; ++k) p->cert_why[k] = p->h_cert->why[k];
+    p->cert_rechecked = 0;
+    p->cert_nan = 0;
+    p->cert_us = 0;
+    const int64_t m = std::min(nflag, cap);
+    if (m > 0) {
+        PU_TRY_HIP(hipMemcpyAsync(flagged, list, (size_t)m * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        PU_TRY_HIP(hipStreamSynchronize(s));
+        std::sort(flagged, flagged + m);
+    }
+    return PU_OK;
+}
+
+int pu_plan_exact_series(pu_plan *p, const void *data, int64_t ld, const int32_t *trials, int64_t m, double *out,
+                         void *stream)
+{
+    int rc = check_data(p, data, ld);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> guard(p->lock.m);
+    PU_REQUIRE(m >= 0 && (m == 0 || (trials && out)), "pu_plan_exact_series: NULL trials / out");
+    if (m == 0) return PU_OK;
+    const int64_t n = p->n, nchan = p->nchan;
+    std::vector<int64_t> sh((size_t)(m * nchan));
+    for (int64_t k = 0; k < m; ++k) {
+        PU_REQUIRE(0 <= trials[k] && trials[k] < p->ndm, "pu_plan_exact_series: trial %d outside [0, %lld)",
+                   trials[k], (long long)p->ndm);
+        std::copy_n(p->shifts.data() + (size_t)trials[k] * nchan, nchan, sh.data() + k * nchan);
+    }
+    for (auto &v : sh) v = ((v % n) + n) % n;
+    hipStream_t s = pu::as_stream(stream);
+    void *d_sh = nullptr;
+    PU_TRY_HIP(hipMallocAsync(&d_sh, sh.size() * sizeof(int64_t), s));
+    rc = pu::hip_check(hipMemcpyAsync(d_sh, sh.data(), sh.size() * sizeof(int64_t), hipMemcpyHostToDevice, s),
+                       "hipMemcpyAsync(exact series shifts)");
+    if (!rc) rc = pu::exact_series(data, p->dtype, nchan, n, ld, reinterpret_cast<const int64_t *>(d_sh), m, out, s);
+    (void)hipFreeAsync(d_sh, s);
+    const int rs = pu::hip_check(hipStreamSynchronize(s), "hipStreamSynchronize(exact series)");
+    return rc ? rc : rs;
+}
+
+int pu_nonfinite_any(const void *data, int dtype, int64_t nrows, int64_t ncols, int64_t ld, int32_t *flag, void *stream)
+{
+    PU_REQUIRE(data && flag, "pu_nonfinite_any: NULL pointer");
+    PU_REQUIRE(nrows >= 0 && ncols >= 0 && ld >= ncols, "pu_nonfinite_any: bad shape");
+    hipStream_t s = pu::as_stream(stream);
+    if (nrows == 0 || ncols == 0) {
+        PU_TRY_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), s));
+        return PU_OK;
+    }
+    return pu::nonfinite_any_async(data, dtype, nrows, ncols, ld, flag, s);
 }
 
 int pu_plan_search(pu_plan *p, const void *data, int64_t ld, double *max_out, double *std_out,

@@ -38,6 +38,10 @@ SIGNATURES = {
     "pu_plan_dedisperse_dm_tile": (_i32, [_vp, _vp, _i64, _i64, _vp, _i64, _vp]),
     "pu_plan_search_tiles": (_i32, [_vp, _vp, _i64, _i64, _i64, _vp, _sz, _vp]),
     "pu_plan_finalize": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "pu_plan_finalize_range": (_i32, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "pu_plan_finalize_range_flagged": (_i32, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _i64, _vp, _vp]),
+    "pu_plan_exact_series": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _vp]),
+    "pu_nonfinite_any": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _vp]),
     "pu_series_stats_workspace_bytes": (_sz, [_i64, _i64]),
     "pu_series_stats": (_i32, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "pu_plan_info": (_i32, [_vp, _vp, _i32]),
@@ -77,7 +81,7 @@ SIGNATURES = {
 INFO_FIELDS = ("ndm", "dm_tiles", "time_tiles", "trials_per_tile", "time_tile", "chans_per_step",
                "row_stride", "lds_bytes", "acc_is_f64", "max_spread", "group", "slots", "stages",
                "slot_bytes", "raw_stride", "exec_adds", "lds_traffic", "cert_rechecked", "cert_nan", "cert_std", "cert_sign",
-               "cert_tie", "cert_us", "kernel")
+               "cert_tie", "cert_us", "kernel", "rec_elem_bytes", "rec_stride")
 KERNEL_NAMES = ("dedisp_kernel", "dedisp_f64_kernel", "dedisp_sub_kernel", "dedisp_sub_kernel (u16 slots)")
 
 
@@ -368,6 +372,65 @@ class Plan:
                                      stream_ptr(stream)), "pu_plan_finalize")
         return out
 
+    def finalize_range(self, workspace, data, trial_begin, trial_end, out=None, stream=None):
+        """``finalize`` of trials [trial_begin, trial_end) only (pu_plan_finalize_range): the
+        outputs are indexed by plan trial (length ndm), only the range is written; the
+        range's records in ``workspace`` must be complete (every time tile)."""
+        self._check_data(data)
+        data = self._rows_aligned(data, stream)
+        out, workspace = self._outs_ws(data.device, out, workspace)
+        check(lib().pu_plan_finalize_range(self._h, ptr(data), data.stride(0), int(trial_begin), int(trial_end),
+                                           ptr(out[0]), ptr(out[1]), ptr(out[2]), ptr(out[3]), ptr(workspace),
+                                           workspace.numel() * workspace.element_size(), stream_ptr(stream)),
+              "pu_plan_finalize_range")
+        return out
+
+    def finalize_range_flagged(self, workspace, trial_begin, trial_end, out=None, device=None, stream=None):
+        """pu_plan_finalize_range_flagged: the fast statistics of trials [begin, end) and the
+        trials certification would recompute, not recomputed: returns (out, flagged int32
+        numpy array of plan trials, count with a non-finite partial)."""
+        t = torch()
+        dev = device if device is not None else workspace.device
+        out, workspace = self._outs_ws(dev, out, workspace)
+        cap = max(0, int(trial_end) - int(trial_begin))
+        flagged = np.zeros(max(1, cap), np.int32)
+        counts = np.zeros(2, np.int64)
+        check(lib().pu_plan_finalize_range_flagged(self._h, int(trial_begin), int(trial_end), ptr(out[0]), ptr(out[1]),
+                                                   ptr(out[2]), ptr(out[3]), ptr(workspace),
+                                                   workspace.numel() * workspace.element_size(),
+                                                   flagged.ctypes.data_as(ctypes.c_void_p), cap,
+                                                   counts.ctypes.data_as(ctypes.c_void_p), stream_ptr(stream)),
+              "pu_plan_finalize_range_flagged")
+        del t
+        return out, flagged[:min(cap, int(counts[0]))].copy(), int(counts[1])
+
+    def exact_series(self, data, trials, out=None, stream=None):
+        """pu_plan_exact_series: float64 channel-order series (len(trials), nsamples) of the
+        given plan trials (exact at the samples whose columns ``data`` holds)."""
+        t = torch()
+        self._check_data(data)
+        data = self._rows_aligned(data, stream)
+        tr = np.ascontiguousarray(trials, dtype=np.int32)
+        if out is None:
+            out = t.empty((tr.size, self.nsamples), dtype=t.float64, device=data.device)
+        elif (out.dtype != t.float64 or not out.is_contiguous() or out.numel() < tr.size * self.nsamples
+              or out.device != data.device):
+            raise ValueError("out must be a contiguous float64 tensor of >= len(trials) x nsamples on the data device")
+        check(lib().pu_plan_exact_series(self._h, ptr(data), data.stride(0), tr.ctypes.data_as(ctypes.c_void_p),
+                                         tr.size, ptr(out), stream_ptr(stream)), "pu_plan_exact_series")
+        return out
+
+    def records(self, workspace):
+        """The per-(trial, time tile) partial records at the start of ``workspace``, as a
+        (ndm, time_tiles, rec_stride) float32 / float64 view (pu_plan_finalize_range)."""
+        t = torch()
+        eb, rs = self.info["rec_elem_bytes"], self.info["rec_stride"]
+        nel = self.ndm * self.info["time_tiles"] * rs
+        dt = {4: t.float32, 8: t.float64}[eb]
+        if workspace.numel() * workspace.element_size() < nel * eb:
+            raise ValueError("workspace smaller than the plan's records")
+        return workspace.view(t.uint8)[:nel * eb].view(dt).view(self.ndm, self.info["time_tiles"], rs)
+
     def cert_info(self):
         """Certification outcome of the last search / finalize: trials recomputed exactly
         and whether the input's NaN / inf rule applied."""
@@ -435,6 +498,18 @@ class Plan:
         check(lib().pu_plan_dedisperse_dm_tile(self._h, ptr(data), data.stride(0), int(dt), ptr(plane),
                                                plane.stride(0), stream_ptr(stream)), "pu_plan_dedisperse_dm_tile")
         return plane
+
+
+def nonfinite_any(x, flag, stream=None):
+    """pu_nonfinite_any: flag (device int32, 1 element) = 1 if the 2-D float tensor x (row
+    stride x.stride(0)) holds NaN / inf, else 0; asynchronous on ``stream``."""
+    require_gpu()
+    code = dtype_code(x.dtype)
+    if x.dim() != 2 or x.stride(1) != 1 or code is None:
+        raise ValueError("nonfinite_any: a 2-D row-major uint8 / float32 / float64 CUDA tensor")
+    check(lib().pu_nonfinite_any(ptr(x), code, x.shape[0], x.shape[1], x.stride(0), ptr(flag), stream_ptr(stream)),
+          "pu_nonfinite_any")
+    return flag
 
 
 def shift_table(nchan, trial_dms, start_freq, bandwidth, sample_time):

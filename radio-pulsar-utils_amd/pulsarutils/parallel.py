@@ -113,12 +113,42 @@ def ready_tiles(plan, landed):
 
 class PlanSearcher:
     """The per-rank work of :func:`pipelined_broadcast_search` on a HIP plan: time-tile
-    range searches as columns land (pu_plan_search_tiles), then pu_plan_finalize."""
+    range searches as columns land (pu_plan_search_tiles), then pu_plan_finalize.  For
+    :func:`tile_sharded_search` also the per-(trial, time tile) records and the finalize
+    of a trial range (pu_plan_finalize_range)."""
 
     def __init__(self, plan, out=None, workspace=None, device=None):
         self.plan = plan
         self.out, self.workspace = plan._outs_ws(device, out, workspace)
         self.ntiles = plan.info["time_tiles"]
+        self.tt_len = plan.info["time_tile"]
+        self.ndm = plan.ndm
+
+    def tile_window(self, tt):
+        return self.plan.tile_window(tt)
+
+    def records(self):
+        return self.plan.records(self.workspace)
+
+    def finalize_range(self, data, lo, hi, stream=None):
+        return self.plan.finalize_range(self.workspace, data, lo, hi, out=self.out, stream=stream)
+
+    def finalize_range_flagged(self, lo, hi, stream=None):
+        return self.plan.finalize_range_flagged(self.workspace, lo, hi, out=self.out, stream=stream)
+
+    def exact_series(self, data, trials, stream=None):
+        return self.plan.exact_series(data, trials, stream=stream)
+
+    def series_stats(self, series, stream=None):
+        from ._hip import series_stats
+        return series_stats(series, stream=stream)
+
+    def nonfinite(self, x, stream=None):
+        import torch
+
+        from ._hip import nonfinite_any
+        flag = torch.zeros(1, dtype=torch.int32, device=x.device)
+        return nonfinite_any(x, flag, stream=stream)
 
     def ready(self, landed):
         return ready_tiles(self.plan, landed)
@@ -323,8 +353,359 @@ def pipelined_broadcast_search(data, plan, out=None, workspace=None, src=0, chun
     return res
 
 
+def interleaved_chunks(nsamples, tt_len, ntiles, world, chunks):
+    """Column ranges of :func:`tile_sharded_search`'s exchange: rank q owns time tiles
+    ``shard_bounds(ntiles, world, q)`` (columns [t0 tt_len, min(n, t1 tt_len))); chunk k is
+    the k-th of ``chunks`` tile-aligned pieces of EVERY rank's slice, so each rank's slice
+    lands at the same pace (1 / chunks of it per exchange).  Depends on the shape only (every
+    rank issues the same collectives).  Returns the non-empty chunks, each a list of
+    (c0, c1)."""
+    n, tt = int(nsamples), int(tt_len)
+    out = [[] for _ in range(max(1, int(chunks)))]
+    for q in range(int(world)):
+        t0, t1 = shard_bounds(ntiles, world, q)
+        for k in range(len(out)):
+            a, b = shard_bounds(t1 - t0, len(out), k)
+            c0, c1 = min(n, (t0 + a) * tt), min(n, (t0 + b) * tt)
+            if c1 > c0:
+                out[k].append((c0, c1))
+    return [c for c in out if c]
+
+
+def ready_by_blocks(landed, tt_len, nsamples, starts, wa, wb):
+    """Tiles (first samples ``starts``) whose read window [start + wa, start + wb) - reduced
+    modulo nsamples, so a window may wrap - lies in landed column blocks; ``landed[j]``:
+    columns [j tt_len, (j + 1) tt_len) have landed."""
+    n, tt = int(nsamples), int(tt_len)
+    P = np.concatenate([[0], np.cumsum(landed.astype(np.int64))])
+    nb = landed.size
+
+    def full(c0, c1):  # columns [c0, c1) within [0, n): every block they touch landed
+        b0, b1 = c0 // tt, np.minimum(nb, -(-c1 // tt))
+        return (c1 <= c0) | (P[b1] - P[b0] == b1 - b0)
+
+    a = starts + wa
+    ln = (starts + wb) - a
+    a = np.mod(a, n)
+    e = a + ln
+    one = full(a, np.minimum(e, n)) & full(np.zeros_like(a), np.maximum(e - n, 0))
+    return np.where(ln >= n, bool(landed.all()), one)
+
+
+def slice_regions(nsamples, tt_len, ntiles, world, wa, wb):
+    """Per rank the columns its time tiles read: (A, L) = the union of the windows
+    [t tt_len + wa, t tt_len + wb) of its tiles t in shard_bounds(ntiles, world, rank), as an
+    unwrapped start A (columns are taken modulo nsamples) and a length L (None: no tiles;
+    L = nsamples and A = 0 when the union covers the whole array)."""
+    n, tt = int(nsamples), int(tt_len)
+    out = []
+    for q in range(int(world)):
+        t0, t1 = shard_bounds(ntiles, world, q)
+        if t1 <= t0:
+            out.append(None)
+            continue
+        a, b = t0 * tt + int(wa), (t1 - 1) * tt + int(wb)
+        out.append((0, n) if b - a >= n else (a, b - a))
+    return out
+
+
+def _cols(c0, c1, n):
+    """Unwrapped columns [c0, c1) (c1 - c0 <= n) as 1-2 ranges within [0, n)."""
+    a = c0 % n
+    e = a + (c1 - c0)
+    return [(a, e)] if e <= n else [(a, n), (0, e - n)]
+
+
+def tile_sharded_search(data, plan, out=None, workspace=None, src=0, chunks=8, group=None, searcher=None,
+                        collective=DEFAULT_COLLECTIVE, phases=None, full_copy=False):
+    """Time-tile sharding: every rank holds the plan of the WHOLE trial grid and searches a
+    contiguous range of its time tiles (``shard_bounds(time_tiles, world, rank)``) while the
+    filterbank is distributed from ``src`` (None: ``data`` is already complete on every
+    rank); the per-(trial, time tile) records then move to the rank that owns each trial
+    (``shard_bounds(ndm, world, rank)``, one all_to_all), and each rank finalizes its own
+    trials - bit for bit the single-GPU search's result, since every record comes from the
+    same kernel and tables and the finalize combines them in the same order.  Returns
+    ((max, std, snr, rebin) indexed by plan trial, only [lo, hi) written; (lo, hi)).
+
+    Why: a DM tile's cost is mostly fixed (slot build, DMA, stage skeleton do
+    not shrink with its trial count), so splitting the DM grid into world slices adds DM
+    tiles (C3: 20 -> 24 at 8 ranks, slowest shard 126 ms against 857 / 8 = 107); splitting
+    the time tiles keeps the whole grid's 20 DM tiles, and each rank does 1 / world of them.
+
+    The exchange (``full_copy`` False, default): ``src`` scatters to every rank only the
+    columns its tiles read (:func:`slice_regions`: its 1 / world of the samples plus the
+    shift halo), in ``chunks`` pieces (:func:`exchange_chunk`'s scatter; ``collective`` is
+    not used), each rank's tiles launched as their windows land; ``data`` then holds only
+    that region on the receivers.  Trials certification flags are recomputed exactly in
+    pieces: every rank computes the float64 channel-order series of the flagged trials at
+    its own samples (pu_plan_exact_series), the pieces are all-gathered and each owner takes
+    pu_series_stats of its trials' whole series (a non-finite input anywhere - every rank
+    scans its own samples - gives every trial the NaN rule, as the one-GPU search).
+    ``full_copy`` True: the whole filterbank goes to every rank (:func:`interleaved_chunks`
+    by ``collective``: each rank's slice advances by 1 / chunks per exchange) and the
+    owner's finalize rechecks from it.
+    ``searcher`` (tests): ``ntiles``, ``tt_len``, ``ndm``, ``tile_window(tt)``,
+    ``tiles(data, b, e, stream)``, ``records()`` ((ndm, ntiles, R) tensor),
+    ``finalize_range(data, lo, hi, stream)`` and, for ``full_copy`` False,
+    ``finalize_range_flagged(lo, hi, stream)``, ``exact_series(data, trials, stream)``,
+    ``series_stats(series, stream)``, ``nonfinite(x, stream)`` (0-d int tensor)."""
+    import contextlib
+
+    import torch
+    import torch.distributed as dist
+    cuda = data.is_cuda
+    dev = data.device
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    if cuda and data.element_size() == 1 and data.shape[1] % 4 == 0 and (data.data_ptr() % 4 or data.stride(0) % 4):
+        raise ValueError("tile-sharded search of 8-bit data needs rows starting on 4-byte boundaries")
+    if collective not in COLLECTIVES:
+        raise ValueError(f"collective must be one of {COLLECTIVES}, got {collective!r}")
+    nchan, n = data.shape
+    if searcher is None:
+        searcher = PlanSearcher(plan, out, workspace, dev)
+    ntt, tt = int(searcher.ntiles), int(searcher.tt_len)
+    my_t0, my_t1 = shard_bounds(ntt, world, rank)
+    my_lo, my_hi = shard_bounds(searcher.ndm, world, rank)
+    exchange = world > 1 and src is not None  # src None: data is already on every rank
+    sliced = exchange and not full_copy
+    if cuda:
+        cur = torch.cuda.current_stream(dev)
+        comm = torch.cuda.Stream(device=dev)
+        comp = torch.cuda.Stream(device=dev)
+        comm.wait_stream(cur)
+        comp.wait_stream(cur)
+    else:
+        cur = comm = comp = None
+    on_comm = (lambda: torch.cuda.stream(comm)) if cuda else contextlib.nullcontext
+    on_comp = (lambda: torch.cuda.stream(comp)) if cuda else contextlib.nullcontext
+    wa, wb = searcher.tile_window(0)
+    starts = np.arange(ntt, dtype=np.int64) * tt
+    mine = np.zeros(ntt, dtype=bool)
+    mine[my_t0:my_t1] = True
+    done = np.zeros(ntt, dtype=bool)
+    if sliced:
+        regions = slice_regions(n, tt, ntt, world, wa, wb)
+        K = max(1, int(chunks))
+        # chunk k: piece k of every rank's region, padded to the widest
+        chunk_list = []
+        for k in range(K):
+            pieces = [None if rg is None else (rg[0] + shard_bounds(rg[1], K, k)[0], rg[0] + shard_bounds(rg[1], K, k)[1])
+                      for rg in regions]
+            w = max((b - a for pc in pieces if pc is not None for a, b in [pc]), default=0)
+            if w > 0:
+                chunk_list.append((pieces, w))
+        width = max((w for _, w in chunk_list), default=1)
+        staging = torch.empty(world * nchan * width, dtype=data.dtype, device=dev) if rank == src else None
+        piece = torch.empty(nchan * width, dtype=data.dtype, device=dev)
+    else:
+        chunk_list = interleaved_chunks(n, tt, ntt, world, chunks if exchange else 1)
+        landed = np.zeros(-(-n // tt), dtype=bool)
+        width = max(sum(c1 - c0 for c0, c1 in ranges) for ranges in chunk_list)
+        slen = -(-nchan * width // world) * world
+        staging = torch.empty(slen, dtype=data.dtype, device=dev) if exchange else None
+        piece = (torch.empty(slen // world, dtype=data.dtype, device=dev)
+                 if exchange and collective == "scatter_allgather" else None)
+    for item in chunk_list:
+        with on_comm():
+            if phases is not None and exchange:
+                phases.mark("exchange", comm)
+            if sliced:
+                pieces, w = item
+                m = nchan * w
+                if rank == src:
+                    for q, pc in enumerate(pieces):
+                        if q == src or pc is None:
+                            continue  # src keeps its own columns
+                        blk = staging[q * m:q * m + nchan * (pc[1] - pc[0])].view(nchan, pc[1] - pc[0])
+                        o = 0
+                        for c0, c1 in _cols(pc[0], pc[1], n):
+                            blk[:, o:o + c1 - c0].copy_(data[:, c0:c1])
+                            o += c1 - c0
+                dist.scatter(piece[:m], list(staging[:world * m].split(m)) if rank == src else None, src=src,
+                             group=group)
+                if phases is not None:
+                    phases.mark("exchange", comm, end=True)
+                    phases.mark("unpack", comm)
+                pc = pieces[rank]
+                if rank != src and pc is not None:
+                    blk = piece[:nchan * (pc[1] - pc[0])].view(nchan, pc[1] - pc[0])
+                    o = 0
+                    for c0, c1 in _cols(pc[0], pc[1], n):
+                        data[:, c0:c1].copy_(blk[:, o:o + c1 - c0])
+                        o += c1 - c0
+                if phases is not None:
+                    phases.mark("unpack", comm, end=True)
+            elif exchange:
+                ranges = item
+                tot = nchan * sum(c1 - c0 for c0, c1 in ranges)
+                blen = -(-tot // world) * world
+                flat = staging[:blen]
+                views, off = [], 0
+                for c0, c1 in ranges:
+                    views.append((flat[off:off + nchan * (c1 - c0)].view(nchan, c1 - c0), c0, c1))
+                    off += nchan * (c1 - c0)
+                if rank == src:
+                    for v, c0, c1 in views:
+                        v.copy_(data[:, c0:c1])
+                exchange_chunk(flat, piece[:blen // world] if piece is not None else None, rank, src, world,
+                               group=group, collective=collective)
+                if phases is not None:
+                    phases.mark("exchange", comm, end=True)
+                    phases.mark("unpack", comm)
+                if rank != src:
+                    for v, c0, c1 in views:
+                        data[:, c0:c1].copy_(v)
+                if phases is not None:
+                    phases.mark("unpack", comm, end=True)
+            ev = None
+            if cuda:
+                ev = torch.cuda.Event()
+                ev.record(comm)
+        if sliced:
+            pc, rg = item[0][rank], regions[rank]
+            if rank == src:
+                ready = np.ones(ntt, dtype=bool)  # the source holds every column from the start
+            elif rg is None:
+                ready = np.zeros(ntt, dtype=bool)
+            elif rg[1] >= n:
+                ready = np.full(ntt, pc is not None and pc[1] >= rg[0] + rg[1])
+            else:
+                top = pc[1] if pc is not None else rg[0]
+                ready = starts + wb - starts[0] <= top
+        else:
+            for c0, c1 in item:
+                landed[c0 // tt:-(-c1 // tt)] = True
+            ready = ready_by_blocks(landed, tt, n, starts, wa - starts[0], wb - starts[0])
+        if cuda:
+            comp.wait_event(ev)
+        ready = ready & mine & ~done
+        idx = np.flatnonzero(ready)
+        if phases is not None:
+            phases.mark("search", comp)
+        for run in np.split(idx, np.flatnonzero(np.diff(idx) != 1) + 1) if idx.size else []:
+            searcher.tiles(data, int(run[0]), int(run[-1]) + 1, stream=comp)
+        if phases is not None:
+            phases.mark("search", comp, end=True)
+        done |= ready
+    if not done[my_t0:my_t1].all():
+        raise RuntimeError("tile-sharded search: time tiles left unsearched")
+    if cuda:
+        for b in (staging, piece):
+            if b is not None:
+                b.record_stream(comm)
+        comp.wait_stream(comm)
+    with on_comp():
+        if world > 1:
+            # every trial's records of my tiles to the trial's owner; mine from every rank
+            if phases is not None:
+                phases.mark("records", comp)
+            rec = searcher.records()
+            R = rec.shape[2]
+            tb = [shard_bounds(ntt, world, q) for q in range(world)]
+            db = [shard_bounds(searcher.ndm, world, q) for q in range(world)]
+            send_parts = [rec[a:b, my_t0:my_t1].reshape(-1) if q != rank else rec.new_empty(0)
+                          for q, (a, b) in enumerate(db)]
+            in_splits = [p.numel() for p in send_parts]
+            out_splits = [0 if q == rank else (my_hi - my_lo) * (t1 - t0) * R for q, (t0, t1) in enumerate(tb)]
+            send = torch.cat(send_parts)
+            recv = rec.new_empty(sum(out_splits))
+            dist.all_to_all_single(recv, send, out_splits, in_splits, group=group)
+            off = 0
+            for q, (t0, t1) in enumerate(tb):
+                if out_splits[q]:
+                    rec[my_lo:my_hi, t0:t1].copy_(recv[off:off + out_splits[q]].view(my_hi - my_lo, t1 - t0, R))
+                off += out_splits[q]
+            if cuda:
+                send.record_stream(comp)
+                recv.record_stream(comp)
+            if phases is not None:
+                phases.mark("records", comp, end=True)
+        if phases is not None:
+            phases.mark("finalize", comp)
+        if sliced:
+            res = _finalize_sliced(searcher, data, my_lo, my_hi, world, rank, ntt, tt, n, group, comp)
+        else:
+            res = searcher.finalize_range(data, my_lo, my_hi, stream=comp)
+        if phases is not None:
+            phases.mark("finalize", comp, end=True)
+    if cuda:
+        if hasattr(searcher, "streams_done"):
+            searcher.streams_done(comp)
+        cur.wait_stream(comm)
+        cur.wait_stream(comp)
+    return res, (my_lo, my_hi)
+
+
+def _finalize_sliced(searcher, data, lo, hi, world, rank, ntt, tt, n, group, stream):
+    """The owner's finalize when each rank holds only its time slice: the fast statistics
+    and the flagged trials (pu_plan_finalize_range_flagged), then - collectively, in the
+    same order on every rank - the NaN rule or the exact recomputation of every rank's
+    flagged trials from the ranks' series pieces (pu_plan_exact_series at the own samples
+    [t0 tt, t1 tt), all_gather, pu_series_stats by the owner).  Matches resolve_flagged's
+    decisions (csrc/dedisperse.hip) bit for bit."""
+    import torch
+    import torch.distributed as dist
+    dev = data.device
+    out, flagged, nnf = searcher.finalize_range_flagged(lo, hi, stream=stream)
+    cnt = torch.tensor([len(flagged), nnf], dtype=torch.int64, device=dev)
+    allc = torch.empty(world * 2, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(allc, cnt, group=group)
+    allc = allc.view(world, 2).cpu().numpy()
+    if allc[:, 0].sum() == 0:
+        return out
+    s0, s1 = (min(n, b * tt) for b in shard_bounds(ntt, world, rank))
+    if allc[:, 1].sum() > 0:
+        # a non-finite partial somewhere: does the input hold NaN / inf (each rank its samples)?
+        flag = searcher.nonfinite(data[:, s0:s1], stream=stream).to(torch.int64).reshape(1)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+        if int(flag.item()):
+            # every trial holds every sample: max = std = NaN, snr = 0, rebin = 0 (as nan_rule)
+            out[0][lo:hi] = float("nan")
+            out[1][lo:hi] = float("nan")
+            out[2][lo:hi] = 0.0
+            out[3][lo:hi] = 0
+            return out
+    mf = int(allc[:, 0].max())
+    mine = torch.full((mf,), -1, dtype=torch.int64, device=dev)
+    if len(flagged):
+        mine[:len(flagged)] = torch.as_tensor(flagged.astype(np.int64), device=dev)
+    allf = torch.empty(world * mf, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(allf, mine, group=group)
+    allf = allf.cpu().numpy()
+    G = allf[allf >= 0].astype(np.int32)  # owners in rank order, each ascending
+    spans = [tuple(min(n, b * tt) for b in shard_bounds(ntt, world, q)) for q in range(world)]
+    wmax = max(b - a for a, b in spans)
+    B = max(1, (1 << 28) // (8 * max(n, wmax * world)))
+    for b0 in range(0, G.size, B):
+        trials = G[b0:b0 + B]
+        m = trials.size
+        ser = searcher.exact_series(data, trials, stream=stream)  # exact at my samples [s0, s1)
+        pc = torch.zeros((m, wmax), dtype=torch.float64, device=dev)
+        pc[:, :s1 - s0] = ser[:, s0:s1]
+        allp = torch.empty((world * m, wmax), dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(allp, pc, group=group)
+        allp = allp.view(world, m, wmax)
+        own = np.flatnonzero((trials >= lo) & (trials < hi))
+        if own.size == 0:
+            continue
+        full = torch.empty((own.size, n), dtype=torch.float64, device=dev)
+        sel = torch.as_tensor(own, device=dev)
+        for q, (a, b) in enumerate(spans):
+            if b > a:
+                full[:, a:b] = allp[q].index_select(0, sel)[:, :b - a]
+        st = searcher.series_stats(full, stream=stream)
+        for k in range(4):
+            out[k][torch.as_tensor(trials[own].astype(np.int64), device=dev)] = st[k]
+    return out
+
+
+DECOMPOSITIONS = ("dm", "time")
+
+
 def sharded_search(data, trial_DMs, nchan, start_freq, bandwidth, sample_time, group=None, acc=None,
-                   compute=None, broadcast=True, src=0, pipelined=False, chunks=8, collective=DEFAULT_COLLECTIVE):
+                   compute=None, broadcast=True, src=0, pipelined=False, chunks=8, collective=DEFAULT_COLLECTIVE,
+                   decomposition="dm"):
     """Distributed ``_dedispersion_search``: returns (max, std, snr, rebin[int32]) numpy arrays
     covering ALL trials, on every rank.
 
@@ -332,6 +713,10 @@ def sharded_search(data, trial_DMs, nchan, start_freq, bandwidth, sample_time, g
     content matters when ``broadcast``).  ``pipelined`` (HIP compute only) overlaps the
     transfer with the search (:func:`pipelined_broadcast_search`); ``collective`` picks
     the transfer (:func:`exchange_chunk`: ``"broadcast"`` or ``"scatter_allgather"``).
+    ``decomposition`` (with ``pipelined``): ``"dm"`` - each rank plans and searches its
+    contiguous trial slice; ``"time"`` - every rank plans the whole grid, searches a slice of
+    its time tiles and finalizes its trial slice (:func:`tile_sharded_search`).  Both
+    return the same bits.
     """
     import torch
     import torch.distributed as dist
@@ -342,7 +727,24 @@ def sharded_search(data, trial_DMs, nchan, start_freq, bandwidth, sample_time, g
     dev = data.device
     chunk = -(-dms.size // world)  # ceil: equal-size gather buffers
     local = torch.zeros((4, chunk), dtype=torch.float64, device=dev)
-    if pipelined and compute is None:
+    if decomposition not in DECOMPOSITIONS:
+        raise ValueError(f"decomposition must be one of {DECOMPOSITIONS}, got {decomposition!r}")
+    if decomposition == "time" and not (pipelined and compute is None):
+        raise ValueError("decomposition='time' needs the pipelined HIP search (pipelined=True, compute=None)")
+    if decomposition == "time":
+        from . import _hip
+        from .dedispersion import _acc_code, _plan_for, _prepare_data
+        if not (data.is_cuda and data.is_contiguous()):
+            raise ValueError("pipelined sharded_search needs a contiguous device tensor (it is written in place)")
+        x = _prepare_data(data)
+        plan = _plan_for(x, lambda: _hip.shift_table(nchan, dms, start_freq, bandwidth, sample_time),
+                         _acc_code(acc), ("dm-grid", dms.tobytes(), float(start_freq), float(bandwidth),
+                                          float(sample_time)))
+        res, (a, b) = tile_sharded_search(x, plan, src=src if broadcast else None, chunks=chunks, group=group,
+                                          collective=collective)
+        for k in range(4):
+            local[k, :hi - lo] = res[k][lo:hi].to(torch.float64)
+    elif pipelined and compute is None:
         from . import _hip
         from .dedispersion import _acc_code, _plan_for, _prepare_data
         if not (data.is_cuda and data.is_contiguous()):

@@ -1,6 +1,6 @@
 """One rank of tests/test_gpu_multirank.py (not collected by pytest: no ``test_`` prefix).
 
-    python tests/mr_worker.py RANK WORLD PORT CASE [COLLECTIVE]
+    python tests/mr_worker.py RANK WORLD PORT CASE [COLLECTIVE [DECOMPOSITION]]
 
 Every rank runs on cuda:0 of the one leased GPU with a ``gloo`` process group (RCCL
 refuses two ranks on one device; gloo's CUDA broadcast / all_gather stage device
@@ -21,6 +21,10 @@ RCCL calls of the product path - broadcast on the communication stream, all_gath
 barrier - with a single rank).
 COLLECTIVE (default broadcast): the chunk exchange of parallel.exchange_chunk -
 ``broadcast`` or ``scatter_allgather`` (the mesh variant, round 5).
+DECOMPOSITION (default dm): ``time`` checks parallel.tile_sharded_search instead (each rank
+its time tiles of the whole grid's plan, the records all_to_all, pu_plan_finalize_range):
+every rank's trial slice == the one-GPU search of the grid, and sharded_search(decomposition
+="time") == that search on every rank.
 Prints ``RANK r OK`` and exits 0, or raises (non-zero exit, traceback on stderr).
 """
 import os
@@ -34,6 +38,7 @@ sys.path[:0] = [os.path.join(REPO, "radio-pulsar-utils_amd"), REPO]
 def main():
     rank, world, port, case = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
     collective = sys.argv[5] if len(sys.argv) > 5 else "broadcast"
+    decomposition = sys.argv[6] if len(sys.argv) > 6 else "dm"
     from dataclasses import replace
 
     import numpy as np
@@ -56,11 +61,24 @@ def main():
         "C5": (CONFIGS["C5"], 500, 5, 0),
         "C5m": (CONFIGS["C5"], 500, 4, 8),
         "C3s": (replace(CONFIGS["C3"], nchan=512, nsamples=1 << 18), 625, 3, 0),
+        # degenerate inputs (time decomposition): all-zero 8-bit data (every trial flagged:
+        # std 0) and float32 data with one NaN (the NaN rule for every trial)
+        "C3z": (replace(CONFIGS["C3"], nchan=512, nsamples=1 << 18), 100, 3, 0),
+        "C5n": (CONFIGS["C5"], 500, 5, 0),
     }[case]
     x_ref = synth.pulsar_filterbank_device(c)  # deterministic: the same bytes on every rank
+    if case == "C3z":
+        x_ref.zero_()
+    elif case == "C5n":
+        x_ref[7, c.nsamples // 3 + 5] = float("nan")
     full = D.dedispersion_plan(c.nchan, c.dmmin, c.dmmax, c.start_freq, c.bandwidth, c.tsamp)
     dms = full[:ntrials]
     garbage = 255 if x_ref.dtype == torch.uint8 else float("nan")
+
+    def same(a, b):  # bit-equal tensors, NaN == NaN
+        if a.is_floating_point():
+            return bool(((a == b) | (a.isnan() & b.isnan())).all())
+        return torch.equal(a, b)
 
     def received():
         return x_ref.clone() if rank == src else torch.full_like(x_ref, garbage)
@@ -69,6 +87,43 @@ def main():
     sh = _hip.shift_table(c.nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
     plan = _hip.Plan(_hip.dtype_code(x_ref.dtype), _hip.PU_ACC_NATIVE, c.nchan, c.nsamples, sh)
     ref = [o.cpu().numpy() for o in plan.search(x_ref)]
+    if decomposition == "time":
+        # ---- time-tile sharding: each rank its time tiles of the whole grid, records to the
+        # trial owners, finalize of the own trials == the one-GPU search of the grid; with the
+        # whole filterbank sent to every rank (full_copy) and with each rank's region only
+        # (flagged trials settled from the ranks' series pieces)
+        rechecked = plan.cert_info()["rechecked"]
+        for full_copy in (True, False):
+            x = received()
+            res, (lo, hi) = parallel.tile_sharded_search(x, plan, src=src, chunks=chunks, collective=collective,
+                                                         full_copy=full_copy)
+            torch.cuda.synchronize()
+            if full_copy:
+                assert same(x, x_ref), f"rank {rank}: received filterbank differs (time)"
+            else:
+                a, ln = parallel.slice_regions(c.nsamples, plan.info["time_tile"], plan.info["time_tiles"], world,
+                                               *plan.tile_window(0))[rank]
+                cols = torch.as_tensor(np.arange(a, a + ln) % c.nsamples, device=x.device)
+                assert same(x[:, cols], x_ref[:, cols]), f"rank {rank}: region differs (time, sliced)"
+            assert (lo, hi) == parallel.shard_bounds(dms.size, world, rank)
+            for k, (a_, b_) in enumerate(zip(ref, res)):
+                np.testing.assert_array_equal(a_[lo:hi], b_[lo:hi].cpu().numpy(),
+                                              err_msg=f"rank {rank} time output {k} full_copy {full_copy}")
+            del res, x
+        x2 = received()
+        mx, sd, snr, win = parallel.sharded_search(x2, dms, c.nchan, c.start_freq, c.bandwidth, c.tsamp,
+                                                   pipelined=True, src=src, chunks=chunks, collective=collective,
+                                                   decomposition="time")
+        torch.cuda.synchronize()
+        for k, got_k in enumerate((mx, sd, snr, win)):
+            np.testing.assert_array_equal(got_k, ref[k], err_msg=f"rank {rank} sharded time output {k}")
+        print(f"rank {rank}: one-GPU search rechecked {rechecked} trials", flush=True)
+        best = int(np.argmax(snr))
+        dist.barrier()
+        dist.destroy_process_group()
+        print(f"RANK {rank} OK case {case} world {world} {backend} {collective} time best DM {dms[best]:.3f} "
+              f"snr {snr[best]:.3f}", flush=True)
+        return
     x = received()
     res = parallel.pipelined_broadcast_search(x, plan, src=src, chunks=chunks, reserve_cus=reserve,
                                               collective=collective)

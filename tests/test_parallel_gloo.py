@@ -220,3 +220,183 @@ def test_pipelined_broadcast_gloo(tmp_path, world, src, n, chunks, smin, smax, d
     for p, out in zip(procs, outs):
         assert p.returncode == 0, out
         assert "ok" in out
+
+
+@pytest.mark.parametrize("n,tt,ntiles,world,chunks", [(1 << 20, 256, 4096, 8, 8), (1000, 256, 4, 3, 2),
+                                                       (50000, 512, 98, 4, 5), (9000, 256, 36, 2, 8)])
+def test_interleaved_chunks_cover(n, tt, ntiles, world, chunks):
+    """The time-tile sharded exchange's chunks: disjoint tile-aligned column ranges that
+    cover [0, n) once; chunk k holds the k-th piece of every rank's slice (so each slice
+    lands at the same pace), and the ranges depend on the shape only."""
+    from pulsarutils.parallel import interleaved_chunks
+    ch = interleaved_chunks(n, tt, ntiles, world, chunks)
+    assert len(ch) <= chunks
+    cover = np.zeros(n, dtype=int)
+    for ranges in ch:
+        for c0, c1 in ranges:
+            assert c0 % tt == 0 and (c1 % tt == 0 or c1 == n) and c1 > c0
+            cover[c0:c1] += 1
+    assert (cover == 1).all()
+    for q in range(world):
+        t0, t1 = shard_bounds(ntiles, world, q)
+        got = [(c0, c1) for ranges in ch for c0, c1 in ranges if t0 * tt <= c0 < max(t1 * tt, t0 * tt + 1)]
+        assert sum(c1 - c0 for c0, c1 in got) == min(n, t1 * tt) - min(n, t0 * tt)
+
+
+def test_ready_by_blocks_matches_columns():
+    """ready_by_blocks (block prefix sums, windows wrapping modulo n) equals the brute-force
+    check of every column of every window."""
+    from pulsarutils.parallel import ready_by_blocks
+    rng = np.random.default_rng(5)
+    for n, tt, wa, wb in [(10000, 256, -300, 900), (4096, 256, 0, 256 + 700), (5000, 512, -10, 5200),
+                          (3000, 256, 17, 400)]:
+        nb = -(-n // tt)
+        ntt = nb
+        starts = np.arange(ntt, dtype=np.int64) * tt
+        for _ in range(20):
+            landed = rng.random(nb) < 0.7
+            got = ready_by_blocks(landed, tt, n, starts, wa, wb)
+            col = np.repeat(landed, tt)[:n]
+            want = np.array([col[np.arange(s + wa, s + wb) % n].all() for s in starts])
+            assert np.array_equal(got, want), (n, tt, wa, wb)
+
+
+TILE_WORKER = textwrap.dedent("""
+    import sys
+    sys.path[:0] = [{pkg!r}, {repo!r}]
+    import numpy as np, torch, torch.distributed as dist
+    from pulsarutils.parallel import shard_bounds, slice_regions, tile_sharded_search
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    nchan, n, tt, ndm = 5, {n}, 256, {ndm}
+    rng = np.random.default_rng(11)
+    full = rng.random((nchan, n))
+    if {nan}:
+        full[2, n // 2 + 3] = np.nan
+    shifts = rng.integers({smin}, {smax} + 1, size=(ndm, nchan))
+
+    def stats(s):
+        return [s.max(), s.std(), s.sum(), int(np.argmax(s))]
+
+    class NumpySearcher:
+        # per-(trial, time tile) records (sum, sum of squares, max) of the circular
+        # shift-and-sum; finalize combines them in tile order (the same bits whatever rank
+        # computed a tile); trials d % 3 == 1 and trials with a non-finite record are
+        # "flagged" and settled from their whole series (exact_series + series_stats)
+        def __init__(self):
+            self.ntiles, self.tt_len, self.ndm = -(-n // tt), tt, ndm
+            self.rec = torch.full((ndm, self.ntiles, 3), float("nan"), dtype=torch.float64)
+            self.count = np.zeros(self.ntiles, dtype=int)
+        def tile_window(self, i):
+            return (i * tt + int(shifts.min()), i * tt + tt + int(shifts.max()))
+        def tiles(self, d, b, e, stream=None):
+            x = d.numpy()
+            for i in range(b, e):
+                t = np.arange(i * tt, min(n, (i + 1) * tt))
+                for dd in range(ndm):
+                    s = sum(x[c, (t + shifts[dd, c]) % n] for c in range(nchan))
+                    self.rec[dd, i] = torch.tensor([s.sum(), (s * s).sum(), s.max()])
+                self.count[i] += 1
+        def records(self):
+            return self.rec
+        def _fast(self, lo, hi):
+            out = [torch.zeros(ndm, dtype=torch.float64) for _ in range(3)] + [torch.zeros(ndm, dtype=torch.int32)]
+            flagged, nnf = [], 0
+            for dd in range(lo, hi):
+                r = self.rec[dd].numpy()
+                s1 = s2 = 0.0
+                for i in range(self.ntiles):
+                    s1 += r[i, 0]
+                    s2 += r[i, 1]
+                out[0][dd], out[1][dd], out[2][dd], out[3][dd] = r[:, 2].max(), s1, s2, dd
+                if not np.isfinite(r).all():
+                    flagged.append(dd)
+                    nnf += 1
+                elif dd % 3 == 1:
+                    flagged.append(dd)
+            return out, np.array(flagged, dtype=np.int32), nnf
+        def finalize_range(self, d, lo, hi, stream=None):
+            out, flagged, nnf = self._fast(lo, hi)
+            if nnf and not np.isfinite(d.numpy()).all():
+                for k, v in enumerate((float("nan"), float("nan"), 0.0, 0)):
+                    out[k][lo:hi] = v
+                return out
+            if len(flagged):
+                st = self.series_stats(self.exact_series(d, flagged))
+                for k in range(4):
+                    out[k][torch.as_tensor(flagged.astype(np.int64))] = st[k]
+            return out
+        def finalize_range_flagged(self, lo, hi, stream=None):
+            return self._fast(lo, hi)
+        def exact_series(self, d, trials, stream=None):
+            x = d.numpy()
+            t = np.arange(n)
+            return torch.from_numpy(np.stack([sum(x[c, (t + shifts[dd, c]) % n] for c in range(nchan))
+                                              for dd in trials]))
+        def series_stats(self, ser, stream=None):
+            st = [stats(r) for r in ser.numpy()]
+            return [torch.tensor([s[k] for s in st], dtype=torch.float64) for k in range(3)] + \
+                [torch.tensor([s[3] for s in st], dtype=torch.int32)]
+        def nonfinite(self, x, stream=None):
+            return torch.tensor(int(not torch.isfinite(x).all()), dtype=torch.int32)
+
+    ref = NumpySearcher()
+    ref.tiles(torch.from_numpy(full), 0, ref.ntiles)
+    want = ref.finalize_range(torch.from_numpy(full), 0, ndm)
+    data = torch.from_numpy(full.copy()) if rank == {src} else torch.full((nchan, n), float("nan"), dtype=torch.float64)
+    s = NumpySearcher()
+    res, (lo, hi) = tile_sharded_search(data, None, src={src}, chunks={chunks}, searcher=s, collective={collective!r},
+                                        full_copy={full_copy})
+    t0, t1 = shard_bounds(s.ntiles, world, rank)
+    assert s.count.sum() == s.count[t0:t1].sum() and (s.count[t0:t1] == 1).all(), s.count
+    for k in range(4):
+        assert np.array_equal(res[k][lo:hi].numpy(), want[k][lo:hi].numpy(), equal_nan=True), (rank, k)
+    if {full_copy}:
+        assert np.array_equal(data.numpy(), full, equal_nan=True)
+    else:
+        a, ln = slice_regions(n, tt, s.ntiles, world, *s.tile_window(0))[rank]
+        cols = np.arange(a, a + ln) % n
+        assert np.array_equal(data.numpy()[:, cols], full[:, cols], equal_nan=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    print("rank", rank, "ok", lo, hi)
+""")
+
+
+@pytest.mark.parametrize("full_copy", [False, True])
+@pytest.mark.parametrize("world,src,n,ndm,chunks,smin,smax,collective,nan", [
+    (2, 0, 6000, 7, 3, 0, 700, "broadcast", False),
+    (3, 2, 5000, 2, 4, 0, 1300, "scatter_allgather", False),
+    (4, 1, 4099, 9, 2, 40, 300, "scatter_allgather", False),
+    (3, 0, 3000, 5, 3, 0, 900, "broadcast", True),
+    (2, 1, 700, 4, 2, 0, 650, "scatter_allgather", False),
+])
+def test_tile_sharded_search_gloo(tmp_path, world, src, n, ndm, chunks, smin, smax, collective, nan, full_copy):
+    """parallel.tile_sharded_search on CPU under gloo, world 2-4, any source rank, receivers
+    starting from NaN: every rank searches exactly its own time tiles and only once their
+    windows (wrapping modulo n) landed; the records all_to_all brings every trial's records
+    to its owner, whose finalize equals the single-process one bit for bit (ranks with no
+    trials included).  full_copy: every rank ends with the source's filterbank; otherwise
+    (the scatter of each rank's region) with its region, the flagged trials settled from the
+    all-gathered series pieces and a NaN anywhere giving every trial the NaN rule."""
+    script = tmp_path / "tile_worker.py"
+    script.write_text(TILE_WORKER.format(pkg=PKG_DIR, repo=REPO, n=n, ndm=ndm, src=src, chunks=chunks, smin=smin,
+                                         smax=smax, collective=collective, nan=nan, full_copy=full_copy))
+    port = _free_port()
+    procs = []
+    for rank in range(world):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                   LOCAL_RANK=str(rank), OMP_NUM_THREADS="1")
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out, _ = p.communicate()
+        outs.append(out)
+    for p, out in zip(procs, outs):
+        assert p.returncode == 0, out
+        assert "ok" in out
