@@ -174,3 +174,69 @@ def test_cached_plan_two_threads(gpu):
         t.join(timeout=120)
     assert not any(t.is_alive() for t in th), "thread hung"
     assert not errors, errors
+
+
+@pytest.mark.parametrize("name,acc", [("C5", "native"), ("C3s", "native"), ("C5", "f64")])
+def test_finalize_range_pieces_equal_full_search(gpu, name, acc):
+    """Round 6 (time-tile sharding): the records of a tile-range search, finalized
+    in trial ranges (pu_plan_finalize_range), equal the one-shot search bit for bit; the
+    deferred form (pu_plan_finalize_range_flagged) writes the same fast statistics and
+    returns the trials the one-shot search's certification recomputed, whose exact series
+    (pu_plan_exact_series) + pu_series_stats give the one-shot outputs; the records view
+    has the documented layout."""
+    import torch
+    from dataclasses import replace
+    c = {"C5": CONFIGS["C5"], "C3s": replace(CONFIGS["C3"], nchan=512, nsamples=1 << 18)}[name]
+    xd = synth.pulsar_filterbank_device(c)
+    dms = D.dedispersion_plan(c.nchan, c.dmmin, c.dmmax, c.start_freq, c.bandwidth, c.tsamp)[:300]
+    sh = _hip.shift_table(c.nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
+    code = {"native": _hip.PU_ACC_NATIVE, "f64": _hip.PU_ACC_F64}[acc]
+    plan = _hip.Plan(_hip.dtype_code(xd.dtype), code, c.nchan, c.nsamples, sh)
+    full = [o.cpu().numpy() for o in plan.search(xd)]
+    ws = torch.empty(plan.workspace_bytes, dtype=torch.uint8, device=xd.device)
+    ntt = plan.info["time_tiles"]
+    plan.search_tiles(xd, 0, ntt // 3, ws)
+    plan.search_tiles(xd, ntt // 3, ntt, ws)
+    rec = plan.records(ws)
+    assert rec.shape == (dms.size, ntt, plan.info["rec_stride"])
+    assert rec.element_size() == plan.info["rec_elem_bytes"]
+    outs = None
+    for lo, hi in [(0, 7), (7, 7), (7, 151), (151, dms.size)]:
+        outs = plan.finalize_range(ws, xd, lo, hi, out=outs)
+    for k in range(4):
+        np.testing.assert_array_equal(outs[k].cpu().numpy(), full[k], err_msg=f"output {k}")
+    # deferred certification: same fast statistics, flagged trials settled by the caller
+    plan.search_tiles(xd, 0, ntt, ws)
+    outs2, flagged, nnf = plan.finalize_range_flagged(ws, 0, dms.size)
+    assert nnf == 0 and np.all(np.diff(flagged) > 0)
+    if flagged.size:
+        ser = plan.exact_series(xd, flagged)
+        st = _hip.series_stats(ser)
+        for k in range(4):
+            outs2[k][torch.as_tensor(flagged.astype(np.int64), device=xd.device)] = st[k]
+    for k in range(4):
+        np.testing.assert_array_equal(outs2[k].cpu().numpy(), full[k], err_msg=f"deferred output {k}")
+
+
+def test_finalize_range_flagged_zero_input_and_nonfinite_scan(gpu):
+    """All-zero input: every trial's std is zero, so every trial of the range is flagged and
+    its exact series is all zeros; pu_nonfinite_any sees a NaN in a column range only when
+    the range holds it."""
+    import torch
+    from dataclasses import replace
+    c = replace(CONFIGS["C3"], nchan=256, nsamples=1 << 16)
+    xd = torch.zeros((c.nchan, c.nsamples), dtype=torch.uint8, device="cuda")
+    dms = D.dedispersion_plan(c.nchan, c.dmmin, c.dmmax, c.start_freq, c.bandwidth, c.tsamp)[:40]
+    sh = _hip.shift_table(c.nchan, dms, c.start_freq, c.bandwidth, c.tsamp)
+    plan = _hip.Plan(_hip.dtype_code(xd.dtype), _hip.PU_ACC_NATIVE, c.nchan, c.nsamples, sh)
+    ws = torch.empty(plan.workspace_bytes, dtype=torch.uint8, device=xd.device)
+    plan.search_tiles(xd, 0, plan.info["time_tiles"], ws)
+    _, flagged, nnf = plan.finalize_range_flagged(ws, 10, 30)
+    assert list(flagged) == list(range(10, 30)) and nnf == 0
+    assert torch.count_nonzero(plan.exact_series(xd, flagged[:3])) == 0
+    xf = torch.ones((16, 1000), dtype=torch.float32, device="cuda")
+    xf[5, 700] = float("nan")
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    assert int(_hip.nonfinite_any(xf[:, 600:800], flag)[0]) == 1
+    assert int(_hip.nonfinite_any(xf[:, :700], flag)[0]) == 0
+    assert int(_hip.nonfinite_any(xd[:, :100], flag)[0]) == 0
