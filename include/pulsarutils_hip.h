@@ -147,11 +147,12 @@ int pu_plan_finalize_range_flagged(pu_plan *plan, int64_t trial_begin, int64_t t
                                    int64_t *counts, void *stream);
 
 /* The reference's float64 dedispersed series (channel order, dedispersion.py:86-98, bit
- * for bit) of m plan trials (host indices) into out (device, m x nsamples contiguous).
- * Sample t reads column (t + shift) mod nsamples of each channel: with only part of the
- * filterbank present, the samples whose columns are present are exact.  Synchronises. */
+ * for bit) of m plan trials (host indices) at samples [t_begin, t_end) into out (device,
+ * m x (t_end - t_begin) contiguous).  Sample t reads column (t + shift) mod nsamples of each
+ * channel: a time-split rank computes its own samples from the columns it holds.
+ * Synchronises. */
 int pu_plan_exact_series(pu_plan *plan, const void *data, int64_t ld, const int32_t *trials, int64_t m,
-                         double *out, void *stream);
+                         int64_t t_begin, int64_t t_end, double *out, void *stream);
 
 /* *flag (device int32) = 1 if any of the nrows x ncols float32 / float64 elements (row
  * stride ld) is NaN or +-inf, else 0 (always 0 for uint8).  Asynchronous on stream. */

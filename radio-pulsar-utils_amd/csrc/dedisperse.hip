@@ -2830,14 +2830,17 @@ int pu_plan_finalize_range_flagged(pu_plan *p, int64_t trial_begin, int64_t tria
     return PU_OK;
 }
 
-int pu_plan_exact_series(pu_plan *p, const void *data, int64_t ld, const int32_t *trials, int64_t m, double *out,
-                         void *stream)
+int pu_plan_exact_series(pu_plan *p, const void *data, int64_t ld, const int32_t *trials, int64_t m, int64_t t_begin,
+                         int64_t t_end, double *out, void *stream)
 {
     int rc = check_data(p, data, ld);
     if (rc) return rc;
     std::lock_guard<std::mutex> guard(p->lock.m);
-    PU_REQUIRE(m >= 0 && (m == 0 || (trials && out)), "pu_plan_exact_series: NULL trials / out");
-    if (m == 0) return PU_OK;
+    PU_REQUIRE(0 <= t_begin && t_begin <= t_end && t_end <= p->n, "pu_plan_exact_series: samples [%lld, %lld) outside [0, %lld)",
+               (long long)t_begin, (long long)t_end, (long long)p->n);
+    PU_REQUIRE(m >= 0, "pu_plan_exact_series: m < 0");
+    if (m == 0 || t_end == t_begin) return PU_OK;
+    PU_REQUIRE(trials && out, "pu_plan_exact_series: NULL trials / out");
     const int64_t n = p->n, nchan = p->nchan;
     std::vector<int64_t> sh((size_t)(m * nchan));
     for (int64_t k = 0; k < m; ++k) {
@@ -2851,7 +2854,9 @@ int pu_plan_exact_series(pu_plan *p, const void *data, int64_t ld, const int32_t
     PU_TRY_HIP(hipMallocAsync(&d_sh, sh.size() * sizeof(int64_t), s));
     rc = pu::hip_check(hipMemcpyAsync(d_sh, sh.data(), sh.size() * sizeof(int64_t), hipMemcpyHostToDevice, s),
                        "hipMemcpyAsync(exact series shifts)");
-    if (!rc) rc = pu::exact_series(data, p->dtype, nchan, n, ld, reinterpret_cast<const int64_t *>(d_sh), m, out, s);
+    if (!rc)
+        rc = pu::exact_series(data, p->dtype, nchan, n, ld, reinterpret_cast<const int64_t *>(d_sh), m, out, s, t_begin,
+                              t_end - t_begin);
     (void)hipFreeAsync(d_sh, s);
     const int rs = pu::hip_check(hipStreamSynchronize(s), "hipStreamSynchronize(exact series)");
     return rc ? rc : rs;

@@ -12,10 +12,11 @@ int nonfinite_any_async(const void *data, int dtype, int64_t nrows, int64_t n, i
                         hipStream_t s);
 
 // The reference's dedispersed series (float64, channel order: bit-identical) of ``rows``
-// trials whose shifts (device, rows x nchan, each reduced to [0, n)) are given, into
-// out (rows x n).  A direct gather: for a handful of trials (certification rechecks).
+// trials whose shifts (device, rows x nchan, each reduced to [0, n)) are given, at samples
+// [t_begin, t_begin + t_len) (t_len < 0: to n) into out (rows x t_len).  A direct gather: for
+// a handful of trials (certification rechecks).
 int exact_series(const void *data, int dtype, int64_t nchan, int64_t n, int64_t ld, const int64_t *shifts, int64_t rows,
-                 double *out, hipStream_t s);
+                 double *out, hipStream_t s, int64_t t_begin = 0, int64_t t_len = -1);
 
 // The reference's result for every trial when the input holds a non-finite value:
 // max = std = NaN, snr = 0, rebin = 0 (dedispersion.py:186-201).

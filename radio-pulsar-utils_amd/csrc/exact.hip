@@ -114,68 +114,188 @@ __global__ void exact_final_kernel(int64_t rows, int64_t n, const uint64_t *__re
 
 // The reference's dedispersed series of a few trials, directly: out[r][t] =
 // ((0 + x[0][(t + s[r][0]) mod n]) + x[1][...]) + ... in float64, channel order
-// (roll_and_sum's order, dedispersion.py:60-98: bit-identical).  The row shifts (in
-// [0, n)) go through LDS 1024 channels at a time.  Every trial reads the whole input
-// once (17 GB at C3: ~4 ms), which is why only flagged trials take this path.
+// (roll_and_sum's order, dedispersion.py:60-98: bit-identical), for samples t in
+// [t_begin, t_begin + t_len) (out rows of t_len).  The row shifts (in [0, n)) go through LDS
+// 1024 channels at a time.  Every trial reads its samples' columns of every channel once
+// (17 GB at C3 for the whole series), which is why only flagged trials take this path.
 //   8-bit: a thread owns 8 consecutive samples and reads them as 3 aligned dwords
-//   (lanes 32 B apart: coalesced), bytes extracted by funnel shifts;
+//   (lanes 8 B apart: coalesced), bytes extracted by funnel shifts;
 //   float: a thread owns samples t0 + l + 64 k (k < 8): every load of a wave is 64
 //   consecutive elements.
+// The loads of U consecutive channels are issued before their adds (which stay in channel
+// order): one channel per iteration waited on its loads every time (13 ms for one trial at
+// C3, latency-bound).
 constexpr int kSeriesPer = 8;
 
 template <typename T>
 __global__ void __launch_bounds__(256)
 exact_series_kernel(const T *__restrict__ x, int64_t ld, int64_t nchan, int64_t n, const int64_t *__restrict__ shifts,
-                    double *__restrict__ out)
+                    double *__restrict__ out, int64_t t_begin, int64_t t_len)
 {
+    constexpr int U = sizeof(T) == 1 ? 8 : sizeof(T) == 4 ? 4 : 2;  // channels in flight
     __shared__ int64_t sh[1024];
     const int64_t r = blockIdx.y;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t t_end = t_begin + t_len;
     // the wave's 512 samples start at w0; this thread's samples
-    const int64_t w0 = ((int64_t)blockIdx.x * 4 + wave) * 64 * kSeriesPer;
+    const int64_t w0 = t_begin + ((int64_t)blockIdx.x * 4 + wave) * 64 * kSeriesPer;
     const int64_t t0 = sizeof(T) == 1 ? w0 + (int64_t)kSeriesPer * lane : w0 + lane;
     const int64_t dt = sizeof(T) == 1 ? 1 : 64;  // sample step between this thread's samples
+    // 8-bit rows read as aligned dwords (x and ld multiples of 4: uniform)
+    const bool rows4 = sizeof(T) == 1 && (reinterpret_cast<uintptr_t>(x) & 3) == 0 && (ld & 3) == 0;
+    const bool full = t0 + (kSeriesPer - 1) * dt < t_end;  // every sample of this thread in range
     double acc[kSeriesPer];
 #pragma unroll
     for (int k = 0; k < kSeriesPer; ++k) acc[k] = 0.0;
+    // one channel's adds, the general way (wrapping windows, partial threads)
+    auto slow = [&](int64_t c, int64_t s) {
+        const T *row = x + c * ld;
+        int64_t idx = t0 + s;
+        while (idx >= n) idx -= n;
+#pragma unroll
+        for (int k = 0; k < kSeriesPer; ++k) {
+            if (t0 + k * dt < t_end) acc[k] += static_cast<double>(row[idx]);
+            idx += dt;
+            while (idx >= n) idx -= n;  // n < 64 may wrap more than once
+        }
+    };
     for (int64_t c0 = 0; c0 < nchan; c0 += 1024) {
         const int64_t nc = nchan - c0 < 1024 ? nchan - c0 : 1024;
         __syncthreads();
         for (int64_t i = threadIdx.x; i < nc; i += 256) sh[i] = shifts[r * nchan + c0 + i];
         __syncthreads();
-        if (w0 >= n) continue;
-        for (int64_t ci = 0; ci < nc; ++ci) {
-            const T *row = x + (c0 + ci) * ld;
-            int64_t idx = t0 + sh[ci];
-            if (idx >= n) idx -= n;
+        if (w0 >= t_end) continue;
+        int64_t ci = 0;
+        for (; ci + U <= nc; ci += U) {
+            int64_t idx[U];
+            bool ok = full;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                idx[u] = t0 + sh[ci + u];
+                if (idx[u] >= n) idx[u] -= n;
+                ok = ok && idx[u] + (sizeof(T) == 1 ? 12 : (kSeriesPer - 1) * 64 + 1) <= n;
+            }
+            if (sizeof(T) == 1) ok = ok && rows4;
+            if (!ok) {
+                for (int u = 0; u < U; ++u) slow(c0 + ci + u, sh[ci + u]);
+                continue;
+            }
             if constexpr (sizeof(T) == 1) {
-                const bool fast = idx + 12 <= n && t0 + kSeriesPer <= n && (reinterpret_cast<uintptr_t>(row) & 3) == 0;
-                if (fast) {
-                    const int64_t a = idx & ~int64_t(3);
-                    const uint32_t *p = reinterpret_cast<const uint32_t *>(row + a);
-                    const uint32_t d0 = p[0], d1 = p[1], d2 = p[2];
-                    const uint32_t sft = (uint32_t)(idx - a) * 8u;
+                uint32_t d[U][3];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t *p = reinterpret_cast<const uint32_t *>(x + (c0 + ci + u) * ld + (idx[u] & ~int64_t(3)));
+                    d[u][0] = p[0];
+                    d[u][1] = p[1];
+                    d[u][2] = p[2];
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t sft = (uint32_t)(idx[u] & 3) * 8u;
                     // bytes idx .. idx + 7 as two dwords (funnel shift across the dwords)
-                    const uint32_t lo = sft ? (d0 >> sft) | (d1 << (32u - sft)) : d0;
-                    const uint32_t hi = sft ? (d1 >> sft) | (d2 << (32u - sft)) : d1;
+                    const uint32_t lo = sft ? (d[u][0] >> sft) | (d[u][1] << (32u - sft)) : d[u][0];
+                    const uint32_t hi = sft ? (d[u][1] >> sft) | (d[u][2] << (32u - sft)) : d[u][1];
 #pragma unroll
                     for (int k = 0; k < 4; ++k) acc[k] += (double)((lo >> (8 * k)) & 0xffu);
 #pragma unroll
                     for (int k = 0; k < 4; ++k) acc[4 + k] += (double)((hi >> (8 * k)) & 0xffu);
-                    continue;
                 }
-            }
+            } else {
+                T v[U][kSeriesPer];
 #pragma unroll
-            for (int k = 0; k < kSeriesPer; ++k) {
-                if (t0 + k * dt < n) acc[k] += static_cast<double>(row[idx]);
-                idx += dt;
-                while (idx >= n) idx -= n;  // n < 64 may wrap more than once
+                for (int u = 0; u < U; ++u) {
+                    const T *row = x + (c0 + ci + u) * ld + idx[u];
+#pragma unroll
+                    for (int k = 0; k < kSeriesPer; ++k) v[u][k] = row[k * 64];
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int k = 0; k < kSeriesPer; ++k) acc[k] += static_cast<double>(v[u][k]);
             }
         }
+        for (; ci < nc; ++ci) slow(c0 + ci, sh[ci]);
     }
 #pragma unroll
     for (int k = 0; k < kSeriesPer; ++k)
-        if (t0 + k * dt < n) out[r * n + t0 + k * dt] = acc[k];
+        if (t0 + k * dt < t_end) out[r * t_len + (t0 + k * dt - t_begin)] = acc[k];
+}
+
+// 8-bit input: the same series from channel segments of kSegChans channels (grid.z), each
+// summed as integers and added into out with float64 atomics.  Every partial sum is an
+// integer below 2^53, so any order of the adds gives the bits of the channel-order float64
+// chain (as colsum_u8_seg_kernel argues for the column sums); the segments give one trial
+// nchan / kSegChans times the workgroups (one trial at C3: 10.7 ms sequential over channels).
+constexpr int kSegChans = 256;
+
+__global__ void __launch_bounds__(256)
+exact_series_u8_seg_kernel(const uint8_t *__restrict__ x, int64_t ld, int64_t nchan, int64_t n,
+                           const int64_t *__restrict__ shifts, double *__restrict__ out, int64_t t_begin, int64_t t_len)
+{
+    constexpr int U = 8;
+    __shared__ int64_t sh[kSegChans];
+    const int64_t r = blockIdx.y;
+    const int64_t c0 = (int64_t)blockIdx.z * kSegChans;
+    const int64_t nc = nchan - c0 < kSegChans ? nchan - c0 : kSegChans;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t t_end = t_begin + t_len;
+    const int64_t w0 = t_begin + ((int64_t)blockIdx.x * 4 + wave) * 64 * kSeriesPer;
+    const int64_t t0 = w0 + (int64_t)kSeriesPer * lane;
+    for (int64_t i = threadIdx.x; i < nc; i += 256) sh[i] = shifts[r * nchan + c0 + i];
+    __syncthreads();
+    if (w0 >= t_end) return;
+    const bool full = t0 + kSeriesPer - 1 < t_end;
+    uint32_t acc[kSeriesPer];  // <= kSegChans x 255 < 2^17
+#pragma unroll
+    for (int k = 0; k < kSeriesPer; ++k) acc[k] = 0;
+    auto slow = [&](int64_t c, int64_t s) {
+        const uint8_t *row = x + c * ld;
+        int64_t idx = t0 + s;
+        while (idx >= n) idx -= n;
+#pragma unroll
+        for (int k = 0; k < kSeriesPer; ++k) {
+            if (t0 + k < t_end) acc[k] += row[idx];
+            idx += 1;
+            if (idx >= n) idx -= n;
+        }
+    };
+    int64_t ci = 0;
+    for (; ci + U <= nc; ci += U) {
+        int64_t idx[U];
+        bool ok = full;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            idx[u] = t0 + sh[ci + u];
+            if (idx[u] >= n) idx[u] -= n;
+            ok = ok && idx[u] + 12 <= n;
+        }
+        if (!ok) {
+            for (int u = 0; u < U; ++u) slow(c0 + ci + u, sh[ci + u]);
+            continue;
+        }
+        uint32_t d[U][3];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t *p = reinterpret_cast<const uint32_t *>(x + (c0 + ci + u) * ld + (idx[u] & ~int64_t(3)));
+            d[u][0] = p[0];
+            d[u][1] = p[1];
+            d[u][2] = p[2];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t sft = (uint32_t)(idx[u] & 3) * 8u;
+            const uint32_t lo = sft ? (d[u][0] >> sft) | (d[u][1] << (32u - sft)) : d[u][0];
+            const uint32_t hi = sft ? (d[u][1] >> sft) | (d[u][2] << (32u - sft)) : d[u][1];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc[k] += (lo >> (8 * k)) & 0xffu;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc[4 + k] += (hi >> (8 * k)) & 0xffu;
+        }
+    }
+    for (; ci < nc; ++ci) slow(c0 + ci, sh[ci]);
+#pragma unroll
+    for (int k = 0; k < kSeriesPer; ++k)
+        if (t0 + k < t_end) unsafeAtomicAdd(out + r * t_len + (t0 + k - t_begin), (double)acc[k]);
 }
 
 template <typename T>
@@ -299,21 +419,31 @@ int nonfinite_any_async(const void *data, int dtype, int64_t nrows, int64_t n, i
 }
 
 int exact_series(const void *data, int dtype, int64_t nchan, int64_t n, int64_t ld, const int64_t *shifts, int64_t rows,
-                 double *out, hipStream_t s)
+                 double *out, hipStream_t s, int64_t t_begin, int64_t t_len)
 {
-    const dim3 grid((unsigned)((n + 4 * 64 * kSeriesPer - 1) / (4 * 64 * kSeriesPer)), (unsigned)rows), blk(256);
+    if (t_len < 0) t_len = n - t_begin;
+    if (t_len <= 0 || rows <= 0) return PU_OK;
+    const dim3 grid((unsigned)((t_len + 4 * 64 * kSeriesPer - 1) / (4 * 64 * kSeriesPer)), (unsigned)rows), blk(256);
     switch (dtype) {
     case PU_U8:
+        if ((reinterpret_cast<uintptr_t>(data) & 3) == 0 && (ld & 3) == 0) {
+            // integer channel segments, float64 atomics (exact: integer sums < 2^53)
+            PU_TRY_HIP(hipMemsetAsync(out, 0, (size_t)rows * (size_t)t_len * sizeof(double), s));
+            const dim3 g3(grid.x, grid.y, (unsigned)((nchan + kSegChans - 1) / kSegChans));
+            hipLaunchKernelGGL(exact_series_u8_seg_kernel, g3, blk, 0, s, reinterpret_cast<const uint8_t *>(data), ld,
+                               nchan, n, shifts, out, t_begin, t_len);
+            return launch_check("exact_series_u8_seg_kernel");
+        }
         hipLaunchKernelGGL(exact_series_kernel<uint8_t>, grid, blk, 0, s, reinterpret_cast<const uint8_t *>(data), ld,
-                           nchan, n, shifts, out);
+                           nchan, n, shifts, out, t_begin, t_len);
         break;
     case PU_F32:
         hipLaunchKernelGGL(exact_series_kernel<float>, grid, blk, 0, s, reinterpret_cast<const float *>(data), ld,
-                           nchan, n, shifts, out);
+                           nchan, n, shifts, out, t_begin, t_len);
         break;
     case PU_F64:
         hipLaunchKernelGGL(exact_series_kernel<double>, grid, blk, 0, s, reinterpret_cast<const double *>(data), ld,
-                           nchan, n, shifts, out);
+                           nchan, n, shifts, out, t_begin, t_len);
         break;
     default: set_error("exact_series: dtype %d", dtype); return PU_EUNSUPPORTED;
     }

@@ -40,7 +40,7 @@ SIGNATURES = {
     "pu_plan_finalize": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "pu_plan_finalize_range": (_i32, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "pu_plan_finalize_range_flagged": (_i32, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _i64, _vp, _vp]),
-    "pu_plan_exact_series": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _vp]),
+    "pu_plan_exact_series": (_i32, [_vp, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp]),
     "pu_nonfinite_any": (_i32, [_vp, _i32, _i64, _i64, _i64, _vp, _vp]),
     "pu_series_stats_workspace_bytes": (_sz, [_i64, _i64]),
     "pu_series_stats": (_i32, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
@@ -404,20 +404,25 @@ class Plan:
         del t
         return out, flagged[:min(cap, int(counts[0]))].copy(), int(counts[1])
 
-    def exact_series(self, data, trials, out=None, stream=None):
-        """pu_plan_exact_series: float64 channel-order series (len(trials), nsamples) of the
-        given plan trials (exact at the samples whose columns ``data`` holds)."""
+    def exact_series(self, data, trials, out=None, stream=None, t_begin=0, t_end=None):
+        """pu_plan_exact_series: float64 channel-order series (len(trials), t_end - t_begin) of
+        the given plan trials at samples [t_begin, t_end) (default: all), exact where the
+        columns they read are in ``data``."""
         t = torch()
         self._check_data(data)
         data = self._rows_aligned(data, stream)
         tr = np.ascontiguousarray(trials, dtype=np.int32)
+        t_end = self.nsamples if t_end is None else int(t_end)
+        w = t_end - int(t_begin)
         if out is None:
-            out = t.empty((tr.size, self.nsamples), dtype=t.float64, device=data.device)
-        elif (out.dtype != t.float64 or not out.is_contiguous() or out.numel() < tr.size * self.nsamples
+            out = t.empty((tr.size, max(0, w)), dtype=t.float64, device=data.device)
+        elif (out.dtype != t.float64 or not out.is_contiguous() or out.numel() < tr.size * w
               or out.device != data.device):
-            raise ValueError("out must be a contiguous float64 tensor of >= len(trials) x nsamples on the data device")
+            raise ValueError("out must be a contiguous float64 tensor of >= len(trials) x (t_end - t_begin) on the "
+                             "data device")
         check(lib().pu_plan_exact_series(self._h, ptr(data), data.stride(0), tr.ctypes.data_as(ctypes.c_void_p),
-                                         tr.size, ptr(out), stream_ptr(stream)), "pu_plan_exact_series")
+                                         tr.size, int(t_begin), t_end, ptr(out), stream_ptr(stream)),
+              "pu_plan_exact_series")
         return out
 
     def records(self, workspace):

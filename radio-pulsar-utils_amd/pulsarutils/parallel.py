@@ -136,8 +136,8 @@ class PlanSearcher:
     def finalize_range_flagged(self, lo, hi, stream=None):
         return self.plan.finalize_range_flagged(self.workspace, lo, hi, out=self.out, stream=stream)
 
-    def exact_series(self, data, trials, stream=None):
-        return self.plan.exact_series(data, trials, stream=stream)
+    def exact_series(self, data, trials, t_begin, t_end, stream=None):
+        return self.plan.exact_series(data, trials, stream=stream, t_begin=t_begin, t_end=t_end)
 
     def series_stats(self, series, stream=None):
         from ._hip import series_stats
@@ -447,7 +447,7 @@ def tile_sharded_search(data, plan, out=None, workspace=None, src=0, chunks=8, g
     ``searcher`` (tests): ``ntiles``, ``tt_len``, ``ndm``, ``tile_window(tt)``,
     ``tiles(data, b, e, stream)``, ``records()`` ((ndm, ntiles, R) tensor),
     ``finalize_range(data, lo, hi, stream)`` and, for ``full_copy`` False,
-    ``finalize_range_flagged(lo, hi, stream)``, ``exact_series(data, trials, stream)``,
+    ``finalize_range_flagged(lo, hi, stream)``, ``exact_series(data, trials, t_begin, t_end, stream)``,
     ``series_stats(series, stream)``, ``nonfinite(x, stream)`` (0-d int tensor)."""
     import contextlib
 
@@ -641,8 +641,8 @@ def _finalize_sliced(searcher, data, lo, hi, world, rank, ntt, tt, n, group, str
     """The owner's finalize when each rank holds only its time slice: the fast statistics
     and the flagged trials (pu_plan_finalize_range_flagged), then - collectively, in the
     same order on every rank - the NaN rule or the exact recomputation of every rank's
-    flagged trials from the ranks' series pieces (pu_plan_exact_series at the own samples
-    [t0 tt, t1 tt), all_gather, pu_series_stats by the owner).  Matches resolve_flagged's
+    flagged trials from the ranks' series pieces (pu_plan_exact_series of the own samples
+    [t0 tt, t1 tt) only, all_gather, pu_series_stats by the owner).  Matches resolve_flagged's
     decisions (csrc/dedisperse.hip) bit for bit."""
     import torch
     import torch.distributed as dist
@@ -680,9 +680,9 @@ def _finalize_sliced(searcher, data, lo, hi, world, rank, ntt, tt, n, group, str
     for b0 in range(0, G.size, B):
         trials = G[b0:b0 + B]
         m = trials.size
-        ser = searcher.exact_series(data, trials, stream=stream)  # exact at my samples [s0, s1)
         pc = torch.zeros((m, wmax), dtype=torch.float64, device=dev)
-        pc[:, :s1 - s0] = ser[:, s0:s1]
+        if s1 > s0:
+            pc[:, :s1 - s0] = searcher.exact_series(data, trials, s0, s1, stream=stream)  # my samples [s0, s1)
         allp = torch.empty((world * m, wmax), dtype=torch.float64, device=dev)
         dist.all_gather_into_tensor(allp, pc, group=group)
         allp = allp.view(world, m, wmax)

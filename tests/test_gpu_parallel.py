@@ -211,6 +211,9 @@ def test_finalize_range_pieces_equal_full_search(gpu, name, acc):
     assert nnf == 0 and np.all(np.diff(flagged) > 0)
     if flagged.size:
         ser = plan.exact_series(xd, flagged)
+        # a sample range is the same samples of the whole series (time-split ranks)
+        n3 = c.nsamples // 3 + 5
+        assert torch.equal(plan.exact_series(xd, flagged, t_begin=n3, t_end=2 * n3), ser[:, n3:2 * n3])
         st = _hip.series_stats(ser)
         for k in range(4):
             outs2[k][torch.as_tensor(flagged.astype(np.int64), device=xd.device)] = st[k]
@@ -234,9 +237,32 @@ def test_finalize_range_flagged_zero_input_and_nonfinite_scan(gpu):
     _, flagged, nnf = plan.finalize_range_flagged(ws, 10, 30)
     assert list(flagged) == list(range(10, 30)) and nnf == 0
     assert torch.count_nonzero(plan.exact_series(xd, flagged[:3])) == 0
+    assert plan.exact_series(xd, flagged[:3], t_begin=100, t_end=100).shape == (3, 0)
     xf = torch.ones((16, 1000), dtype=torch.float32, device="cuda")
     xf[5, 700] = float("nan")
     flag = torch.zeros(1, dtype=torch.int32, device="cuda")
     assert int(_hip.nonfinite_any(xf[:, 600:800], flag)[0]) == 1
     assert int(_hip.nonfinite_any(xf[:, :700], flag)[0]) == 0
     assert int(_hip.nonfinite_any(xd[:, :100], flag)[0]) == 0
+
+
+@pytest.mark.parametrize("dt", ["u8", "f32", "f64"])
+def test_exact_series_ranges_equal_oracle_rows(gpu, dt):
+    """pu_plan_exact_series (the certification recompute; loads of 8/4/2 channels issued ahead
+    of their adds, round 6) equals the oracle's float64 channel-order rows bit for bit, over
+    the whole series and over sample ranges that start and end anywhere (ragged n, windows
+    wrapping modulo n)."""
+    import torch
+    n, nchan = 70001, 37
+    rng = np.random.default_rng(7)
+    x = {"u8": rng.integers(0, 256, (nchan, n)).astype(np.uint8), "f32": rng.random((nchan, n)).astype(np.float32),
+         "f64": rng.random((nchan, n))}[dt]
+    xd = torch.from_numpy(x).cuda()
+    dms = np.linspace(0.0, 400.0, 9)
+    sh = _hip.shift_table(nchan, dms, 1200.0, 300.0, 64e-6)
+    plan = _hip.Plan(_hip.dtype_code(xd.dtype), _hip.PU_ACC_F64, nchan, n, sh)
+    want = np.stack([oracle.dedisperse(x, sh[d]) for d in range(dms.size)])
+    tr = np.arange(dms.size, dtype=np.int32)
+    np.testing.assert_array_equal(plan.exact_series(xd, tr).cpu().numpy(), want)
+    for a, b in [(0, 1), (5, 4100), (n - 700, n), (12345, 12346 + 8 * 513)]:
+        np.testing.assert_array_equal(plan.exact_series(xd, tr, t_begin=a, t_end=b).cpu().numpy(), want[:, a:b])

@@ -328,9 +328,9 @@ TILE_WORKER = textwrap.dedent("""
             return out
         def finalize_range_flagged(self, lo, hi, stream=None):
             return self._fast(lo, hi)
-        def exact_series(self, d, trials, stream=None):
+        def exact_series(self, d, trials, t_begin=0, t_end=n, stream=None):
             x = d.numpy()
-            t = np.arange(n)
+            t = np.arange(t_begin, t_end)
             return torch.from_numpy(np.stack([sum(x[c, (t + shifts[dd, c]) % n] for c in range(nchan))
                                               for dd in trials]))
         def series_stats(self, ser, stream=None):
