@@ -675,7 +675,11 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
     const i32x4 tile = ld_uniform(tiles + dt);        // {first trial, count, raw row length, copy bytes}
     const i32x2 ts = ld_uniform(tile_stages + dt);    // {first stage, stage count}
     const int first = tile.x, cnt = tile.y;
-    const int copy_bytes = tile.w;
+    // alignment-copy bytes: float32 slots share the tile's (its widest span: whole build
+    // passes need no store guards, C2's 2560 B at UP = 10); a 16-bit slot's follow from its
+    // own length (the planner sizes it by its own span: (len + 2) u16, 64-rounded)
+    const int tile_copy_bytes = tile.w;
+    auto copy_bytes_of = [&](int len) { return S16 ? ((len + 65) & ~63) * 2 : tile_copy_bytes; };
     const int slot0 = wave * D;
     const bool active = slot0 < cnt;
     const int n = o.n;
@@ -792,7 +796,7 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
     // the allocation returns 0 (clamping them costs a VALU add per read - the reads then
     // cannot fold 256 u into the ds_read offset field - and was measured 1.8 ms slower at
     // C2, 20.2 vs 18.4 ms).
-    auto build_pass = [&](auto upc, const meta_t &m, int gs, int i0, int lim, bool whole) {
+    auto build_pass = [&](auto upc, const meta_t &m, int gs, int i0, int lim, bool whole, int copy_bytes) {
         constexpr int UP = decltype(upc)::value;
         auto at = [&](int u) { return i0 + 64 * u + lane; };
         float r[UP];
@@ -889,6 +893,7 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
     // summed.
     auto slot16_pairs = [&](const meta_t &m) {
         const bool four = m[0] > 384;
+        const int copy_bytes = copy_bytes_of(m[0]);
         auto odd = [&](uint32_t e, uint32_t enext) {  // (R[2k + 1], R[2k + 2]) of lane k
             const uint32_t x = (uint32_t)__builtin_amdgcn_mov_dpp((int)enext, 0x134, 0xf, 0xf, false);  // wave_rol:1
             const uint32_t y = (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)e, 0x130, 0xf, 0xf, false);  // wave_shl:1
@@ -935,6 +940,7 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
 
     auto slot16_quad = [&](const meta_t &m) {
         const int len = m[0];  // 256 (= TT) .. 510
+        const int copy_bytes = copy_bytes_of(len);
         auto odd = [&](uint32_t e, uint32_t enext) {  // (R[2k + 1], R[2k + 2]) of lane k
             const uint32_t x = (uint32_t)__builtin_amdgcn_mov_dpp((int)enext, 0x134, 0xf, 0xf, false);  // wave_rol:1
             const uint32_t y = (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)e, 0x130, 0xf, 0xf, false);  // wave_shl:1
@@ -1018,8 +1024,9 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
     // slot over waves to balance the ~20 slots of a stage over 16 waves was measured
     // slower: 22.1 / 25.6 vs 20.2 ms for halves / thirds - fewer reads in flight per
     // pass, and the extra pass code spilled registers.)
-    auto pass_whole = [&](int i0) { return copy_bytes % (256 * U) == 0 || 4 * i0 + 256 * U <= copy_bytes; };
-    const bool whole0 = pass_whole(0);  // the first pass of every slot of the tile
+    auto pass_whole = [&](int i0, int copy_bytes) {
+        return copy_bytes % (256 * U) == 0 || 4 * i0 + 256 * U <= copy_bytes;
+    };
     auto build = [&](const i32x4 st, const meta_t m0) {
         // the next slot's record is loaded a slot ahead (round 5: loaded on demand, its
         // scalar-load latency stood in front of every slot after a wave's first), through a
@@ -1031,9 +1038,10 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
         auto slot = [&](const meta_t &m) {
             const int len = m[0], gs = m[3];
             const int lim = (len + 63) & ~63;
-            build_pass(std::integral_constant<int, U>{}, m, gs, 0, lim, whole0);
+            const int cb = copy_bytes_of(len);
+            build_pass(std::integral_constant<int, U>{}, m, gs, 0, lim, pass_whole(0, cb), cb);
             for (int i0 = 64 * U; i0 < len; i0 += 64 * U)
-                build_pass(std::integral_constant<int, U>{}, m, gs, i0, lim, pass_whole(i0));
+                build_pass(std::integral_constant<int, U>{}, m, gs, i0, lim, pass_whole(i0, cb), cb);
         };
         meta_t ma = m0;
         const meta_t *mp = reinterpret_cast<const meta_t *>(slots) + (size_t)(st.z + wave + W);
@@ -2042,7 +2050,17 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     std::vector<i32x2> tile_stages((size_t)ndt);
     std::vector<int32_t> slotmeta, base;
     std::vector<uint32_t> rec((size_t)ndt * ngroups * W * D);
-    std::vector<int64_t> slot_local((size_t)ngroups), slot_base((size_t)ngroups);
+    std::vector<int64_t> slot_base((size_t)ngroups);
+    std::vector<std::vector<int64_t>> slot_off((size_t)ngroups);  // per group: each slot's byte offset
+    // 16-bit slots' alignment copies are sized by their own span (round 6; the tile's widest
+    // span sized every slot before): more groups per stage
+    // (16-bit slots only: float32 slots keep the tile's size, see sub_item's copy_bytes_of)
+    auto slot_copy = [&](size_t t, const SubSlot &sl) { return copy_of(s16 ? sl.hi - sl.lo : span_t[t]); };
+    auto group_slot_bytes = [&](size_t t, int g) {
+        int64_t b = 0;
+        for (const auto &sl : tslots[t * ngroups + g]) b += ncopies * slot_copy(t, sl);
+        return b;
+    };
     int64_t prev_slots = 0;
     // element offset of a stage's first raw row: its rows end at the top of LDS
     auto raw_top_f = [&](int g0, int g1) {
@@ -2091,10 +2109,10 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
                 int64_t u = 0, ch = 0;
                 while (g_stop < ngroups) {
                     const int gs = (int)std::min<int64_t>(G, nchan - (int64_t)g_stop * G);
-                    const int64_t ns = (int64_t)tslots[(size_t)t * ngroups + g_stop].size();
+                    const int64_t nb = group_slot_bytes((size_t)t, g_stop);
                     const int64_t rb = raw_bytes(ch + gs, raw_stride);
-                    if (g_stop > g && (rb + (u + ns) * ncopies * cb > stage_cap || rb + prev_slots > stage_cap)) break;
-                    u += ns;
+                    if (g_stop > g && (rb + u + nb > stage_cap || rb + prev_slots > stage_cap)) break;
+                    u += nb;
                     ch += gs;
                     ++g_stop;
                 }
@@ -2102,15 +2120,17 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
                     pu::set_error("subband mode: consecutive stages do not fit the LDS budget");
                     return PU_EUNSUPPORTED;
                 }
-                prev_slots = u * ncopies * cb;
+                prev_slots = u;
             }
             int g_end = g;
             while (g_end < g_stop) {
                 const int64_t c0 = (int64_t)g_end * G;
                 const int gs = (int)std::min<int64_t>(G, nchan - c0);
                 const auto &sls = tslots[(size_t)t * ngroups + g_end];
-                slot_local[g_end] = used;
+                slot_off[g_end].clear();
                 for (const auto &sl : sls) {
+                    const int64_t cbs = slot_copy((size_t)t, sl);
+                    slot_off[g_end].push_back(used);
                     // 16-bit slots: len = the elements the windows read (the build's chunk count)
                     const int64_t len = TT + (sl.hi - sl.lo) + (s16 ? 0 : 1);
                     adds_tile += len * gs;
@@ -2119,7 +2139,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
                     else
                         lds_tile += ((len + 63) / 64 * 64) * (dma ? eb * G + 8 : 8);  // build reads + 2 writes
                     slotmeta.push_back((int32_t)len);
-                    slotmeta.push_back((int32_t)(zr + used * ncopies * cb));
+                    slotmeta.push_back((int32_t)(zr + used));
                     slotmeta.push_back((int32_t)c0);
                     slotmeta.push_back(gs);
                     for (int k = 0; k < ms - 4; ++k) {
@@ -2137,7 +2157,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
                         }
                         slotmeta.push_back((int32_t)src);
                     }
-                    ++used;
+                    used += ncopies * cbs;
                 }
                 chans += gs;
                 ++g_end;
@@ -2145,7 +2165,7 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
             stages.push_back(i32x4{g, g_end, s_begin, (int32_t)(slotmeta.size() / ms)});
             tile_stages[t][1]++;
             if (dma) lds_tile += chans * ((row_len * eb + 255) / 256 * 256);  // DMA writes
-            slot_used = std::max(slot_used, zr + used * ncopies * cb);
+            slot_used = std::max(slot_used, zr + used);
             for (int gg = g; gg < g_end; ++gg) slot_base[gg] = zr;
             max_stage_chans = std::max(max_stage_chans, chans);
             g = g_end;
@@ -2160,9 +2180,10 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
                     size_t si = 0;
                     while (sls[si].vid != v) ++si;
                     const int64_t rr = S(tr, (int64_t)gg * G) - sls[si].lo;
+                    const int64_t cbs = slot_copy((size_t)t, sls[si]);
                     // copy rr mod 2 (float32) / rr mod 4 (u16), the aligned element below rr
-                    r[d] = (uint32_t)(slot_base[gg] + (slot_local[gg] + (int64_t)si) * ncopies * cb +
-                                      (s16 ? (rr & 3) * cb + (rr & ~int64_t(3)) * 2 : (rr & 1) * cb + (rr & ~int64_t(1)) * 4));
+                    r[d] = (uint32_t)(slot_base[gg] + slot_off[gg][si] +
+                                      (s16 ? (rr & 3) * cbs + (rr & ~int64_t(3)) * 2 : (rr & 1) * cbs + (rr & ~int64_t(1)) * 4));
                 }
             }
         }
@@ -2545,6 +2566,16 @@ int pu_plan_create_ex(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t 
         auto cost = [](const pu_plan *q) {
             return (double)q->lds_traffic + 3.0e6 * (double)q->nstages * q->ntt + 200.0 * (double)q->cost_windows16;
         };
+        // Round 6, per-slot copy sizes for 16-bit slots: fewer stages for both G, G = 8 most
+        // (C3 5000 trials tall G = 4 855.9 -> 847.2 ms, G = 8 936.7 -> 885.3; the 625-trial
+        // shard G = 8 114.1 -> 111.9), and the cost above then ranks tall G = 8 first at 5000
+        // trials too - wrongly.  Between the two tall 16-bit-slot plans a stage costs 6e6
+        // B-equivalents, inside the (4.5e6, 1.0e7) that ranks both measurements right; the
+        // winner meets the other shapes under the cost above (6e6 for every plan would pick
+        // the wide float32 plan at C3: 1066 vs 847 ms).
+        auto cost_tall16 = [](const pu_plan *q) {
+            return (double)q->lds_traffic + 6.0e6 * (double)q->nstages * q->ntt + 200.0 * (double)q->cost_windows16;
+        };
         auto fresh = [&]() {
             pu_plan *q = new pu_plan();
             q->dtype = p->dtype;
@@ -2578,9 +2609,11 @@ int pu_plan_create_ex(pu_plan **out, int dtype, int acc, int64_t nchan, int64_t 
                 return r;
             }
         }
-        pu_plan *keep = nullptr;
-        for (auto [cand, ok] : {std::pair<pu_plan *, bool>{p, rc4 == PU_OK}, {q, rc8 == PU_OK}, {t4, rct4 == PU_OK},
-                                {t8, rct8 == PU_OK}})
+        pu_plan *keep = nullptr, *tall = nullptr;
+        if (rct4 == PU_OK && rct8 == PU_OK && t4->slot16 && t8->slot16)
+            tall = cost_tall16(t8) < cost_tall16(t4) ? t8 : t4;
+        for (auto [cand, ok] : {std::pair<pu_plan *, bool>{p, rc4 == PU_OK}, {q, rc8 == PU_OK},
+                                {t4, rct4 == PU_OK && (!tall || tall == t4)}, {t8, rct8 == PU_OK && (!tall || tall == t8)}})
             if (ok && (!keep || cost(cand) < cost(keep))) keep = cand;
         for (pu_plan *cand : {p, q, t4, t8})  // losers (p stays when nothing fits: it is reused below)
             if (cand != keep && (keep || cand != p)) free_plan(cand);

@@ -34,7 +34,9 @@ for v in variants:
     saved = {k: os.environ.get(k) for k in kv}
     os.environ.update(kv)
     acc = {"native": _hip.PU_ACC_NATIVE, "f32": _hip.PU_ACC_F32, "f64": _hip.PU_ACC_F64}[os.environ.get("AB_ACC", "native")]
-    plans[v] = _hip.Plan(_hip.dtype_code(x.dtype), acc, cfg.nchan, cfg.nsamples, sh)
+    plans[v] = _hip.Plan(_hip.dtype_code(x.dtype), acc, cfg.nchan, cfg.nsamples, sh,
+                         group=int(os.environ.get("AB_GROUP", "0")),  # AB_GROUP / AB_SHAPE: pin the plan
+                         shape=int(os.environ["AB_SHAPE"]) if "AB_SHAPE" in os.environ else None)
     for k, val in saved.items():
         if val is None:
             os.environ.pop(k, None)
