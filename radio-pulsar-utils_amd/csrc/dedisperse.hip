@@ -679,7 +679,12 @@ __device__ __forceinline__ void sub_item(SubArgs &a, const i32x4 *__restrict__ t
     // passes need no store guards, C2's 2560 B at UP = 10); a 16-bit slot's follow from its
     // own length (the planner sizes it by its own span: (len + 2) u16, 64-rounded)
     const int tile_copy_bytes = tile.w;
-    auto copy_bytes_of = [&](int len) { return S16 ? ((len + 65) & ~63) * 2 : tile_copy_bytes; };
+    auto copy_bytes_of = [&](int len) {
+        if constexpr (S16) return ((len + 65) & ~63) * 2;
+        // float32: whole build passes (64 U elements: no store guards), at most the tile's
+        const int whole = (len + 64 * U) / (64 * U) * (64 * U) * 4;
+        return whole < tile_copy_bytes ? whole : tile_copy_bytes;
+    };
     const int slot0 = wave * D;
     const bool active = slot0 < cnt;
     const int n = o.n;
@@ -2054,8 +2059,14 @@ int plan_sub(pu_plan *p, const int64_t *shifts, int G, int shape, size_t budget)
     std::vector<std::vector<int64_t>> slot_off((size_t)ngroups);  // per group: each slot's byte offset
     // 16-bit slots' alignment copies are sized by their own span (round 6; the tile's widest
     // span sized every slot before): more groups per stage
-    // (16-bit slots only: float32 slots keep the tile's size, see sub_item's copy_bytes_of)
-    auto slot_copy = [&](size_t t, const SubSlot &sl) { return copy_of(s16 ? sl.hi - sl.lo : span_t[t]); };
+    // 16-bit slots by their own span; float32 slots by theirs rounded up to whole build passes
+    // of 64 U elements (sub_item's U), at most the tile's size (sub_item's copy_bytes_of)
+    const int64_t UP64 = 64 * std::min<int64_t>((TT + 80 + 63) / 64, (p->dtype == PU_F64 ? 20 : 40) / G);
+    auto slot_copy = [&](size_t t, const SubSlot &sl) {
+        if (s16) return copy_of(sl.hi - sl.lo);
+        const int64_t whole = (TT + (sl.hi - sl.lo) + 2 + UP64 - 1) / UP64 * UP64 * 4;
+        return std::min(whole, copy_of(span_t[t]));
+    };
     auto group_slot_bytes = [&](size_t t, int g) {
         int64_t b = 0;
         for (const auto &sl : tslots[t * ngroups + g]) b += ncopies * slot_copy(t, sl);
